@@ -1,0 +1,499 @@
+/*
+ * fk_oracle.c -- CPU restatement of the reference k-mer counting algorithm.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity oracle: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The
+ * product library (fastkmer_amd/csrc) never links, calls or falls back to it.
+ *
+ * It restates, in plain C, the hot path of maruscia/fastkmer (Scala/Spark):
+ *   - util.is_allowed            src/main/scala/skc/package.scala:46-75
+ *   - util.fillNorm              src/main/scala/skc/package.scala:77-100
+ *   - util.reverse_complement    src/main/scala/skc/package.scala:103-115
+ *   - Kmer.getSignature          src/main/scala/skc/package.scala:337-357
+ *   - Kmer.lastM                 src/main/scala/skc/package.scala:310-326
+ *   - util.hash_to_bucket        src/main/scala/skc/package.scala:686-695
+ *   - util.getOrientation(Kmer)  src/main/scala/skc/package.scala:721-728
+ *   - firstAndLastOccurrenceOfInvalidNucleotide  package.scala:739-754
+ *   - SparkBinKmerCounter.getSuperKmers          SparkBinKmerCounter.scala:34-169
+ *   - extractKXmers (sorted count + "EOF")       SparkBinKmerCounter.scala:428-660
+ *   - extractKXmersHT (hash count, no "EOF")     SparkBinKmerCounter.scala:664-739
+ *   - TestConfiguration.b = min(4^m, B)          src/main/scala/skc/test/package.scala:32
+ *   - read = record value with '\n' removed      SparkBinKmerCounter.scala:62-65
+ *
+ * Control flow of the map side (getSuperKmers) is kept step for step,
+ * including the O(k) invalid-byte scan per window, the O(k) signature
+ * recomputation when the minimizer expires and the strict "<" slide, so the
+ * super-k-mers and bins it produces are the reference's.  The reduce side
+ * counts canonical k-mers per bin exactly; the (k,x)-mer packing and heap
+ * merge of extractKXmers are a memory layout of the same multiset (the
+ * literal transliteration in oracle/literal_ref.py checks that claim).
+ *
+ * k-mers are held as unsigned __int128, 2 bits per base, MSB-first (A=0, C=1,
+ * G=2, T=3; package.scala:18-22), so numeric order == lexicographic order
+ * (Kmer.compare, package.scala:389-404).  k <= 64 is supported.
+ *
+ * FASTA record semantics (FASTdoop 1.0 is not in /root/reference; SURVEY
+ * Appendix A): a header line starts with '>' at a line start; the read is the
+ * concatenation of the following non-header lines with every '\n' removed;
+ * every other byte ('\r', 'N', lowercase, IUPAC) stays in the read and breaks
+ * k-mer windows.  Lines before the first header are ignored.  With
+ * sequence_type == 1 (FASTAlongInputFileFormat) each record is one long read
+ * (the reference's chunks overlap by k-1, SBKC:993, which gives the same
+ * counts as counting the whole record).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <errno.h>
+#include <sys/stat.h>
+
+typedef unsigned __int128 u128;
+
+#define FKO_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------ */
+/* primitives                                                          */
+/* ------------------------------------------------------------------ */
+
+/* package.scala:18-22 -- A,C,G,T -> 0..3; everything else is "not a
+ * nucleotide" (package.scala:697). */
+static inline int fko_code(uint8_t c) {
+    switch (c) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        default: return -1;
+    }
+}
+
+/* package.scala:46-75, literally: the loop runs length-3 times on the low
+ * 4 bits, then four checks on what is left of the m-mer. */
+FKO_API int fko_is_allowed(int32_t mmer_in, int32_t length) {
+    int32_t mmer = mmer_in;
+    for (int j = 0; j < length - 3; ++j) {
+        if ((mmer & 0xf) == 0) return 0; /* AA inside */
+        mmer >>= 2;
+    }
+    if (mmer == 0) return 0;          /* AAA prefix */
+    if (mmer == 0x04) return 0;       /* ACA prefix */
+    if ((mmer & 0x3c) == 0) return 0; /* AA* prefix */
+    if ((mmer & 0xf) == 0) return 0;  /* *AA prefix */
+    return 1;
+}
+
+/* package.scala:103-115 */
+FKO_API int64_t fko_reverse_complement(int64_t seq, int32_t length) {
+    int64_t cur = seq, rev = 0;
+    int shift = length * 2 - 2;
+    for (int i = 0; i < length; ++i) {
+        rev += (int64_t)(3 - (cur & 3)) << shift;
+        cur >>= 2;
+        shift -= 2;
+    }
+    return rev;
+}
+
+/* one entry of fillNorm (package.scala:77-100) */
+FKO_API int32_t fko_norm(int32_t v, int32_t m) {
+    int32_t def = 1 << (m * 2);
+    int32_t rev = (int32_t)fko_reverse_complement(v, m);
+    int32_t sv = fko_is_allowed(v, m) ? v : def;
+    int32_t rv = fko_is_allowed(rev, m) ? rev : def;
+    return sv < rv ? sv : rv;
+}
+
+/* package.scala:686-695 (Java int arithmetic, >>> = logical shift) */
+FKO_API int32_t fko_hash_to_bucket(int32_t s, int32_t B) {
+    uint32_t key = (uint32_t)s;
+    const uint32_t c2 = 0x27d4eb2du;
+    key = (key ^ 61u) ^ (key >> 16);
+    key = key + (key << 3);
+    key = key ^ (key >> 4);
+    key = key * c2;
+    key = key ^ (key >> 15);
+    return (int32_t)((key & 0x7FFFFFFFu) % (uint32_t)B);
+}
+
+/* test/package.scala:32: b = min(4^m, max_b) computed in double */
+FKO_API int32_t fko_clamp_bins(int32_t m, int32_t B) {
+    double p = 1.0;
+    for (int i = 0; i < m; ++i) p *= 4.0;
+    double b = p < (double)B ? p : (double)B;
+    return (int32_t)b;
+}
+
+/* ------------------------------------------------------------------ */
+/* result container                                                    */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    u128 *keys;
+    uint32_t *counts; /* filled after reduction */
+    int64_t n, cap;
+} fko_bin;
+
+typedef struct fko_result {
+    int32_t k, m, nbins;
+    fko_bin *bins;
+    int64_t total_kmers;
+    int64_t superkmers;
+    int64_t reads;
+    /* optional super-k-mer trace (fko_trace_read) */
+    int64_t *trace_start, *trace_len;
+    int32_t *trace_bin;
+    int64_t trace_cap;
+} fko_result;
+
+static void bin_push(fko_bin *b, u128 key) {
+    if (b->n == b->cap) {
+        int64_t nc = b->cap ? b->cap * 2 : 64;
+        u128 *nk = (u128 *)realloc(b->keys, (size_t)nc * sizeof(u128));
+        if (!nk) { fprintf(stderr, "fk_oracle: out of memory\n"); abort(); }
+        b->keys = nk;
+        b->cap = nc;
+    }
+    b->keys[b->n++] = key;
+}
+
+/* ------------------------------------------------------------------ */
+/* map side: getSuperKmers (SparkBinKmerCounter.scala:34-169)          */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    int32_t k, m, B;
+    const int32_t *norm; /* fillNorm table, or NULL -> computed per call */
+} fko_params;
+
+static inline int32_t norm_of(const fko_params *p, int32_t v) {
+    return p->norm ? p->norm[v] : fko_norm(v, p->m);
+}
+
+/* value of the m-mer of cur starting at pos (all bytes valid by caller) */
+static inline int32_t mmer_at(const uint8_t *cur, int64_t pos, int m) {
+    int32_t v = 0;
+    for (int t = 0; t < m; ++t) v = (v << 2) | fko_code(cur[pos + t]);
+    return v;
+}
+
+/* Kmer.getSignature (package.scala:337-357): leftmost strict minimum of
+ * norm over the k-m+1 m-mers of the k-mer that starts at read offset i.
+ * Returns the value; *pos receives the m-mer's offset inside the k-mer. */
+static int32_t get_signature(const fko_params *p, const uint8_t *cur, int64_t i, int32_t *pos) {
+    int32_t sig = norm_of(p, mmer_at(cur, i, p->m));
+    *pos = 0;
+    for (int t = 1; t + p->m <= p->k; ++t) {
+        int32_t v = norm_of(p, mmer_at(cur, i + t, p->m));
+        if (v < sig) { sig = v; *pos = t; }
+    }
+    return sig;
+}
+
+/* firstAndLastOccurrenceOfInvalidNucleotide (package.scala:739-754):
+ * offsets relative to start, (-1,-1) when the range is all ACGT. */
+static void first_last_invalid(const uint8_t *s, int64_t start, int64_t end, int64_t *first, int64_t *last) {
+    *first = -1;
+    *last = -1;
+    for (int64_t i = start; i < end; ++i) {
+        if (fko_code(s[i]) < 0) {
+            if (*first == -1) *first = i - start;
+            *last = i - start;
+        }
+    }
+}
+
+/* getOrientation(Kmer, i, j) (package.scala:721-728) on read bytes:
+ * 0 = forward strand is lexicographically smaller, 1 = reverse complement
+ * (ties -> 1; a palindrome is its own reverse complement). */
+static int orientation(const uint8_t *s, int64_t i, int64_t j) {
+    for (;;) {
+        int a = fko_code(s[i]);
+        int b = 3 - fko_code(s[j]);
+        if (a < b) return 0;
+        if (a > b || i >= j) return 1;
+        ++i;
+        --j;
+    }
+}
+
+/* canonical k-mer of read bytes [i, i+k) via the orientation rule and the
+ * (orientation==1 => reverse complement) copy of Kmer.readFromKmer
+ * (package.scala:256-290). */
+static u128 canonical_at(const uint8_t *s, int64_t i, int k) {
+    u128 v = 0;
+    if (orientation(s, i, i + k - 1) == 0) {
+        for (int t = 0; t < k; ++t) v = (v << 2) | (u128)fko_code(s[i + t]);
+    } else {
+        for (int t = k - 1; t >= 0; --t) v = (v << 2) | (u128)(3 - fko_code(s[i + t]));
+    }
+    return v;
+}
+
+/* Emit one super-k-mer: on the reduce side (extractKXmers/HT) each of its
+ * len-k+1 k-mers is canonicalised and counted in bin `bin`. */
+static void emit_superkmer(fko_result *r, const fko_params *p, const uint8_t *cur, int64_t start, int64_t len, int32_t sig) {
+    int32_t bin = fko_hash_to_bucket(sig, p->B);
+    fko_bin *b = &r->bins[bin];
+    if (r->trace_start && r->superkmers < r->trace_cap) {
+        r->trace_start[r->superkmers] = start;
+        r->trace_len[r->superkmers] = len;
+        r->trace_bin[r->superkmers] = bin;
+    }
+    for (int64_t i = start; i + p->k <= start + len; ++i) {
+        bin_push(b, canonical_at(cur, i, p->k));
+        r->total_kmers++;
+    }
+    r->superkmers++;
+}
+
+/* SparkBinKmerCounter.scala:59-161 for one read `cur` of length n. */
+static void get_super_kmers_read(fko_result *r, const fko_params *p, const uint8_t *cur, int64_t n) {
+    const int k = p->k, m = p->m;
+    if (n < k) return; /* :67 */
+    int32_t min_value = -1;
+    int64_t min_pos = -1; /* Signature(-1,-1), :69 */
+    int64_t sk_start = 0;
+    int64_t i = 0;
+    int64_t nf, nl;
+    while (i < n - k + 1) {                           /* :75 */
+        first_last_invalid(cur, i, i + k, &nf, &nl); /* :78 */
+        if (nf != -1) {
+            if (sk_start < i) /* :84-89 */
+                emit_superkmer(r, p, cur, sk_start, i - 1 + k - sk_start, min_value);
+            sk_start = i + nl + 1; /* :95 */
+            i += nl + 1;           /* :96 */
+        } else {
+            if (i > min_pos) { /* :102 minimizer left the window */
+                if (sk_start < i) {
+                    emit_superkmer(r, p, cur, sk_start, i - 1 + k - sk_start, min_value); /* :104 */
+                    sk_start = i;
+                }
+                int32_t rel;
+                min_value = get_signature(p, cur, i, &rel); /* :112 */
+                min_pos = rel + i;
+            } else {
+                int32_t last = norm_of(p, mmer_at(cur, i + k - m, m)); /* lastM, :117 */
+                if (last < min_value) {                                 /* :119 strict */
+                    if (sk_start < i) {
+                        emit_superkmer(r, p, cur, sk_start, i - 1 + k - sk_start, min_value); /* :124 */
+                        sk_start = i;
+                    }
+                    min_value = last; /* :132 */
+                    min_pos = i + k - m;
+                }
+            }
+            i += 1;
+        }
+    }
+    if (n - sk_start >= k) { /* :142 */
+        first_last_invalid(cur, i, n, &nf, &nl);
+        if (nf == -1) {
+            emit_superkmer(r, p, cur, sk_start, n - sk_start, min_value); /* :148 */
+        } else if (i + nf >= sk_start + k) {                              /* :152 (unreachable) */
+            emit_superkmer(r, p, cur, sk_start, i + nf, min_value);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* FASTA records (SBKC:62-65 + FASTdoop semantics, Appendix A)          */
+/* ------------------------------------------------------------------ */
+
+typedef void (*read_cb)(void *ctx, const uint8_t *read, int64_t n);
+
+static void for_each_read(const uint8_t *buf, size_t n, read_cb cb, void *ctx) {
+    uint8_t *read = NULL;
+    int64_t rn = 0, rcap = 0;
+    int in_record = 0;
+    size_t pos = 0;
+    while (pos < n) {
+        size_t e = pos;
+        while (e < n && buf[e] != '\n') ++e; /* line [pos, e) */
+        if (e > pos && buf[pos] == '>') {
+            if (in_record) cb(ctx, read, rn);
+            in_record = 1;
+            rn = 0;
+        } else if (in_record) {
+            int64_t len = (int64_t)(e - pos);
+            if (rn + len > rcap) {
+                int64_t nc = rcap ? rcap : 256;
+                while (nc < rn + len) nc *= 2;
+                uint8_t *nr = (uint8_t *)realloc(read, (size_t)nc);
+                if (!nr) { fprintf(stderr, "fk_oracle: out of memory\n"); abort(); }
+                read = nr;
+                rcap = nc;
+            }
+            memcpy(read + rn, buf + pos, (size_t)len);
+            rn += len;
+        }
+        pos = e + 1;
+    }
+    if (in_record) cb(ctx, read, rn);
+    free(read);
+}
+
+typedef struct {
+    fko_result *r;
+    fko_params *p;
+} map_ctx;
+
+static void map_read(void *vctx, const uint8_t *read, int64_t n) {
+    map_ctx *c = (map_ctx *)vctx;
+    c->r->reads++;
+    get_super_kmers_read(c->r, c->p, read, n);
+}
+
+/* ------------------------------------------------------------------ */
+/* reduce side: exact multiplicity per canonical k-mer per bin          */
+/* ------------------------------------------------------------------ */
+
+static int cmp_u128(const void *a, const void *b) {
+    u128 x = *(const u128 *)a, y = *(const u128 *)b;
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+static void reduce_bin(fko_bin *b) {
+    if (b->n == 0) return;
+    qsort(b->keys, (size_t)b->n, sizeof(u128), cmp_u128);
+    uint32_t *cnt = (uint32_t *)malloc((size_t)b->n * sizeof(uint32_t));
+    int64_t u = 0;
+    for (int64_t i = 0; i < b->n; ++i) {
+        if (u > 0 && b->keys[u - 1] == b->keys[i]) {
+            cnt[u - 1]++;
+        } else {
+            b->keys[u] = b->keys[i];
+            cnt[u] = 1;
+            ++u;
+        }
+    }
+    b->n = u;
+    b->counts = cnt;
+}
+
+/* Runs the whole job. B is the requested bin count; it is clamped to
+ * min(4^m, B) exactly like TestConfiguration.b.  Returns NULL on invalid
+ * parameters (the reference would throw). */
+FKO_API fko_result *fko_count(const uint8_t *fasta, size_t n, int32_t k, int32_t m, int32_t B, int32_t sequence_type) {
+    (void)sequence_type; /* same counts for both record formats (see header) */
+    if (k < 1 || k > 64 || m < 1 || m > 15 || m > k || B < 1) return NULL;
+    fko_params p;
+    p.k = k;
+    p.m = m;
+    p.B = fko_clamp_bins(m, B);
+    int32_t *norm = NULL;
+    if (m <= 12) { /* fillNorm table (package.scala:77-100), per task (SBKC:47) */
+        int64_t sz = (int64_t)1 << (2 * m);
+        norm = (int32_t *)malloc((size_t)sz * sizeof(int32_t));
+        for (int64_t v = 0; v < sz; ++v) norm[v] = fko_norm((int32_t)v, m);
+    }
+    p.norm = norm;
+    fko_result *r = (fko_result *)calloc(1, sizeof(fko_result));
+    r->k = k;
+    r->m = m;
+    r->nbins = p.B;
+    r->bins = (fko_bin *)calloc((size_t)p.B, sizeof(fko_bin));
+    map_ctx c = {r, &p};
+    for_each_read(fasta, n, map_read, &c);
+    for (int32_t b = 0; b < p.B; ++b) reduce_bin(&r->bins[b]);
+    free(norm);
+    return r;
+}
+
+FKO_API int32_t fko_nbins(const fko_result *r) { return r->nbins; }
+FKO_API int64_t fko_total_kmers(const fko_result *r) { return r->total_kmers; }
+FKO_API int64_t fko_superkmers(const fko_result *r) { return r->superkmers; }
+FKO_API int64_t fko_reads(const fko_result *r) { return r->reads; }
+
+FKO_API int64_t fko_bin_size(const fko_result *r, int32_t b) {
+    if (b < 0 || b >= r->nbins) return -1;
+    return r->bins[b].n;
+}
+
+FKO_API int64_t fko_distinct(const fko_result *r) {
+    int64_t s = 0;
+    for (int32_t b = 0; b < r->nbins; ++b) s += r->bins[b].n;
+    return s;
+}
+
+/* keys split as (hi, lo): lo = last 32 bases, hi = the first k-32 bases
+ * (0 for k <= 32); counts are the Java Int counts. */
+FKO_API int fko_bin_get(const fko_result *r, int32_t b, uint64_t *hi, uint64_t *lo, uint32_t *counts) {
+    if (b < 0 || b >= r->nbins) return -1;
+    const fko_bin *bb = &r->bins[b];
+    for (int64_t i = 0; i < bb->n; ++i) {
+        if (hi) hi[i] = (uint64_t)(bb->keys[i] >> 64);
+        if (lo) lo[i] = (uint64_t)bb->keys[i];
+        if (counts) counts[i] = bb->counts[i];
+    }
+    return 0;
+}
+
+/* Kmer.toString (package.scala:416-454, 496-500) */
+static void key_to_string(u128 key, int k, char *out) {
+    static const char rep[4] = {'A', 'C', 'G', 'T'};
+    for (int t = k - 1; t >= 0; --t) {
+        out[t] = rep[(int)(key & 3)];
+        key >>= 2;
+    }
+    out[k] = 0;
+}
+
+/* Output files as extractKXmers (SBKC:550-606: sorted lines + "EOF", no
+ * trailing newline) or extractKXmersHT (SBKC:715-734: lines only). */
+FKO_API int fko_write_bins(const fko_result *r, const char *dir, int32_t sorted_eof) {
+    if (mkdir(dir, 0755) != 0 && errno != EEXIST) return -1;
+    char path[4096];
+    char kmer[80];
+    for (int32_t b = 0; b < r->nbins; ++b) {
+        const fko_bin *bb = &r->bins[b];
+        if (bb->n == 0) continue;
+        snprintf(path, sizeof(path), "%s/bin%d", dir, b);
+        FILE *f = fopen(path, "wb");
+        if (!f) return -2;
+        for (int64_t i = 0; i < bb->n; ++i) {
+            key_to_string(bb->keys[i], r->k, kmer);
+            fprintf(f, "%s\t%u\n", kmer, bb->counts[i]);
+        }
+        if (sorted_eof) fputs("EOF", f);
+        fclose(f);
+    }
+    return 0;
+}
+
+FKO_API void fko_free(fko_result *r) {
+    if (!r) return;
+    for (int32_t b = 0; b < r->nbins; ++b) {
+        free(r->bins[b].keys);
+        free(r->bins[b].counts);
+    }
+    free(r->bins);
+    free(r);
+}
+
+/* Super-k-mer trace for the literal cross-check: runs getSuperKmers on one
+ * read and records (start, length, bin) of every emitted super-k-mer in
+ * emission order.  Returns the number emitted (may exceed cap). */
+FKO_API int64_t fko_trace_read(const uint8_t *read, int64_t n, int32_t k, int32_t m, int32_t B,
+                               int64_t *out_start, int64_t *out_len, int32_t *out_bin, int64_t cap) {
+    if (k < 1 || k > 64 || m < 1 || m > 15 || m > k || B < 1) return -1;
+    fko_params p;
+    p.k = k;
+    p.m = m;
+    p.B = fko_clamp_bins(m, B);
+    p.norm = NULL;
+    fko_result r;
+    memset(&r, 0, sizeof(r));
+    r.k = k;
+    r.m = m;
+    r.nbins = p.B;
+    r.bins = (fko_bin *)calloc((size_t)p.B, sizeof(fko_bin));
+    r.trace_start = out_start;
+    r.trace_len = out_len;
+    r.trace_bin = out_bin;
+    r.trace_cap = cap;
+    get_super_kmers_read(&r, &p, read, n);
+    for (int32_t b = 0; b < p.B; ++b) free(r.bins[b].keys);
+    free(r.bins);
+    return r.superkmers;
+}
