@@ -1,0 +1,321 @@
+"""fastkmer_amd -- MI355X-native exact k-mer counter (host-side mirror).
+
+The compute path is the HIP library ``fastkmer_amd/lib/libfastkmer.so``
+(C-ABI in ``include/fastkmer.h``); this module binds it with ctypes and
+mirrors the reference's driver-side API:
+
+* :class:`TestConfiguration`  -- skc.test.testutil.TestConfiguration
+  (src/main/scala/skc/test/package.scala:16-42)
+* :func:`execute_job`         -- SparkBinKmerCounter.executeJob
+  (src/main/scala/skc/SparkBinKmerCounter.scala:989-1046)
+* :class:`KmerCounter`        -- the map / shuffle / reduce hot path as one
+  device-resident object (getSuperKmers :34-169, reduceByKey :1035,
+  extractKXmers :428-660, extractKXmersHT :664-739)
+
+There is no CPU fallback: without the built library, or without a GPU,
+constructing a :class:`KmerCounter` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+import re
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libfastkmer.so")
+CLI_PATH = os.path.join(_PKG, "bin", "fastkmer-cli")
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "fastkmer.h")
+
+FK_OK = 0
+ERRORS = {-1: "FK_E_INVALID", -2: "FK_E_STATE", -3: "FK_E_DEVICE", -4: "FK_E_NOMEM", -5: "FK_E_IO",
+          -6: "FK_E_RANGE"}
+
+
+class FastKmerError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {message}")
+        self.code = code
+
+
+class fk_config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("k", "m", "x", "B", "use_ht", "sequence_type", "write", "n_ranks", "rank", "device")]
+
+
+class fk_stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("fasta_bytes", "positions", "bases", "kmers", "superkmers", "records_received", "distinct",
+                 "oversize_buckets")] + \
+               [(n, ctypes.c_double) for n in
+                ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
+                 "ms_signature_kernel")]
+
+
+_lib = None
+
+
+def header_functions() -> list[str]:
+    """Names of the functions declared in include/fastkmer.h."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return re.findall(r"^[A-Za-z_][\w \*]*?\b(fk_\w+)\s*\(", text, re.M)
+
+
+def lib():
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m fastkmer_amd.build` "
+                           "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, U64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "fk_abi_version": (ctypes.c_int, []),
+        "fk_config_init": (ctypes.c_int, [ctypes.POINTER(fk_config)]),
+        "fk_config_validate": (ctypes.c_int, [ctypes.POINTER(fk_config)]),
+        "fk_clamped_bins": (I32, [I32, I32]),
+        "fk_output_dir": (ctypes.c_int, [ctypes.POINTER(fk_config), ctypes.c_char_p, ctypes.c_char_p,
+                                         ctypes.c_char_p, SZ]),
+        "fk_record_bytes_for_k": (SZ, [I32]),
+        "fk_synth_record_bytes": (U64, [I32]),
+        "fk_synth_fasta_host": (ctypes.c_int, [P, U64, U64, I32, U64, U64, ctypes.c_double, ctypes.c_double]),
+        "fk_create": (ctypes.c_int, [ctypes.POINTER(fk_config), ctypes.POINTER(P)]),
+        "fk_destroy": (None, [P]),
+        "fk_last_error": (ctypes.c_char_p, []),
+        "fk_set_stream": (ctypes.c_int, [P, P]),
+        "fk_ingest": (ctypes.c_int, [P, ctypes.c_char_p, SZ, ctypes.c_int]),
+        "fk_ingest_device": (ctypes.c_int, [P, P, SZ, ctypes.c_int]),
+        "fk_synth_fasta_device": (ctypes.c_int, [P, U64, U64, I32, U64, U64, ctypes.c_double, ctypes.c_double]),
+        "fk_map": (ctypes.c_int, [P, P]),
+        "fk_record_bytes": (SZ, [P]),
+        "fk_map_emit": (ctypes.c_int, [P, P, U64]),
+        "fk_reduce": (ctypes.c_int, [P, P, U64]),
+        "fk_finish": (ctypes.c_int, [P]),
+        "fk_num_bins": (I32, [P]),
+        "fk_bin_sizes": (ctypes.c_int, [P, P]),
+        "fk_get_bin": (ctypes.c_int, [P, I32, P, P, SZ, ctypes.POINTER(SZ)]),
+        "fk_write_bins": (ctypes.c_int, [P, ctypes.c_char_p]),
+        "fk_get_stats": (ctypes.c_int, [P, ctypes.POINTER(fk_stats)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != FK_OK:
+        raise FastKmerError(rc, lib().fk_last_error().decode(errors="replace"))
+
+
+def make_config(k: int, m: int, x: int = 3, B: int = 2048, use_ht: bool = False, sequence_type: int = 0,
+                write: bool = False, n_ranks: int = 1, rank: int = 0, device: int = -1) -> fk_config:
+    c = fk_config()
+    lib().fk_config_init(ctypes.byref(c))
+    c.k, c.m, c.x, c.B = k, m, x, B
+    c.use_ht, c.sequence_type, c.write = int(bool(use_ht)), sequence_type, int(bool(write))
+    c.n_ranks, c.rank, c.device = n_ranks, rank, device
+    return c
+
+
+def validate(**kw) -> None:
+    """Host-only configuration check (no GPU); raises FastKmerError."""
+    c = make_config(**kw)
+    _check(lib().fk_config_validate(ctypes.byref(c)))
+
+
+def clamped_bins(m: int, B: int) -> int:
+    return lib().fk_clamped_bins(m, B)
+
+
+def record_bytes_for_k(k: int) -> int:
+    return lib().fk_record_bytes_for_k(k)
+
+
+def synth_fasta(n_reads: int, read_len: int = 100, genome_len: int = 1_000_000, seed: int = 0x5EED,
+                err_rate: float = 0.002, n_rate: float = 0.0005, first_read: int = 0) -> bytes:
+    """Deterministic synthetic short-read FASTA (byte-identical to the device generator)."""
+    L = lib()
+    nb = n_reads * L.fk_synth_record_bytes(read_len)
+    buf = ctypes.create_string_buffer(max(nb, 1))
+    _check(L.fk_synth_fasta_host(buf, first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate))
+    return buf.raw[:nb]
+
+
+def decode_keys(keys: np.ndarray, k: int) -> list[str]:
+    """2-bit keys (one word for k <= 32, (hi, lo) pairs for k > 32) -> strings."""
+    out = []
+    words = keys.reshape(-1, 2) if k > 32 else keys.reshape(-1, 1)
+    for row in words:
+        v = (int(row[0]) << 64) | int(row[1]) if k > 32 else int(row[0])
+        s = []
+        for _ in range(k):
+            s.append("ACGT"[v & 3])
+            v >>= 2
+        out.append("".join(reversed(s)))
+    return out
+
+
+@dataclasses.dataclass
+class TestConfiguration:
+    """Mirror of skc.test.testutil.TestConfiguration (test/package.scala:16-42)."""
+    __test__ = False  # not a pytest class
+
+    dataset: str
+    outputDirectory: str
+    k: int
+    m: int
+    x: int
+    max_b: int = 2000
+    sequenceType: int = 0
+    canonical: bool = True
+    debug: bool = False
+    write: bool = True
+    useKryoSerializer: bool = False
+    useHT: bool = False
+    useCustomPartitioner: bool = False
+    numPartitionTasks: int = 0
+    prefix: str = ""
+
+    @property
+    def b(self) -> int:  # :32
+        return int(min(4.0 ** self.m, float(self.max_b)))
+
+    @property
+    def outputDir(self) -> str:  # :33
+        base = "/tmp/" if self.debug else self.outputDirectory
+        tail = f"{self.prefix}k{self.k}_m{self.m}_x{self.x}_b{self.b}"
+        return base + tail if self.debug else base + tail + f"_s{self.sequenceType}"
+
+
+class KmerCounter:
+    """Device-resident exact canonical k-mer counter for one rank."""
+
+    def __init__(self, k: int, m: int, x: int = 3, B: int = 2048, use_ht: bool = False, sequence_type: int = 0,
+                 n_ranks: int = 1, rank: int = 0, device: int = -1):
+        L = lib()
+        self.k, self.m, self.x, self.use_ht = k, m, x, bool(use_ht)
+        self.n_ranks, self.rank = n_ranks, rank
+        self._cfg = make_config(k, m, x, B, use_ht, sequence_type, False, n_ranks, rank, device)
+        h = ctypes.c_void_p()
+        _check(L.fk_create(ctypes.byref(self._cfg), ctypes.byref(h)))
+        self._h = h
+        self.num_bins = L.fk_num_bins(h)
+        self.record_bytes = L.fk_record_bytes(h)
+        self._keep = None
+        self._sizes = None
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().fk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- input
+    def ingest(self, fasta: bytes) -> None:
+        self._keep = bytes(fasta)
+        _check(lib().fk_ingest(self._h, self._keep, len(self._keep), 1))
+
+    def ingest_device(self, ptr: int, n: int) -> None:
+        _check(lib().fk_ingest_device(self._h, ctypes.c_void_p(ptr), n, 1))
+
+    def synth_device(self, n_reads: int, read_len: int = 100, genome_len: int = 100_000_000, seed: int = 0x5EED,
+                     err_rate: float = 0.002, n_rate: float = 0.0005, first_read: int = 0) -> int:
+        _check(lib().fk_synth_fasta_device(self._h, first_read, n_reads, read_len, genome_len, seed, err_rate,
+                                           n_rate))
+        return n_reads * lib().fk_synth_record_bytes(read_len)
+
+    def set_stream(self, stream_ptr: int) -> None:
+        _check(lib().fk_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
+
+    # -- map / shuffle / reduce
+    def map(self) -> list[int]:
+        self._sizes = None
+        counts = (ctypes.c_uint64 * self.n_ranks)()
+        _check(lib().fk_map(self._h, counts))
+        return list(counts)
+
+    def map_emit(self, dst_ptr: int, cap_records: int) -> None:
+        _check(lib().fk_map_emit(self._h, ctypes.c_void_p(dst_ptr), cap_records))
+
+    def reduce(self, src_ptr: int, n_records: int) -> None:
+        self._sizes = None
+        _check(lib().fk_reduce(self._h, ctypes.c_void_p(src_ptr), n_records))
+
+    def finish(self) -> None:
+        self._sizes = None
+        _check(lib().fk_finish(self._h))
+
+    # -- results
+    def bin_sizes(self) -> np.ndarray:
+        out = np.zeros(self.num_bins, dtype=np.uint64)
+        _check(lib().fk_bin_sizes(self._h, out.ctypes.data))
+        return out
+
+    def get_bin(self, b: int):
+        n = ctypes.c_size_t(0)
+        if self._sizes is None:
+            self._sizes = self.bin_sizes()
+        cnt = int(self._sizes[b])
+        kw = 2 if self.k > 32 else 1
+        keys = np.zeros(max(cnt, 1) * kw, dtype=np.uint64)
+        counts = np.zeros(max(cnt, 1), dtype=np.uint32)
+        _check(lib().fk_get_bin(self._h, b, keys.ctypes.data, counts.ctypes.data, max(cnt, 1), ctypes.byref(n)))
+        return keys[:n.value * kw], counts[:n.value]
+
+    def bin_dict(self, b: int) -> dict:
+        keys, counts = self.get_bin(b)
+        return dict(zip(decode_keys(keys, self.k), (int(c) for c in counts)))
+
+    def all_dict(self) -> dict:
+        sizes = self.bin_sizes()
+        return {b: self.bin_dict(b) for b in np.nonzero(sizes)[0].tolist()}
+
+    def bin_text(self, b: int) -> str:
+        keys, counts = self.get_bin(b)
+        lines = [f"{s}\t{int(c)}\n" for s, c in zip(decode_keys(keys, self.k), counts)]
+        return "".join(lines) + ("" if self.use_ht else "EOF")
+
+    def write_bins(self, out_dir: str) -> None:
+        _check(lib().fk_write_bins(self._h, out_dir.encode()))
+
+    def stats(self) -> dict:
+        st = fk_stats()
+        _check(lib().fk_get_stats(self._h, ctypes.byref(st)))
+        return {n: getattr(st, n) for n, _ in fk_stats._fields_}
+
+
+def execute_job(configuration: TestConfiguration) -> KmerCounter:
+    """SparkBinKmerCounter.executeJob (SparkBinKmerCounter.scala:989-1046) on one GPU.
+
+    Reads the dataset, counts, and writes ``configuration.outputDir/bin<b>``
+    when ``configuration.write`` is set.  Returns the counter (results stay
+    device resident until it is closed).
+    """
+    with open(configuration.dataset, "rb") as f:
+        data = f.read()
+    kc = KmerCounter(configuration.k, configuration.m, configuration.x, configuration.max_b,
+                     configuration.useHT, configuration.sequenceType)
+    kc.ingest(data)
+    kc.finish()
+    if configuration.write:
+        kc.write_bins(configuration.outputDir)
+    return kc

@@ -1,0 +1,834 @@
+// fk_api.cpp -- C-ABI of the MI355X k-mer counter (include/fastkmer.h).
+//
+// Host orchestration of the device pipeline in fk_kernels.hip.  Replaces the
+// body of SparkBinKmerCounter.executeJob (SparkBinKmerCounter.scala:989-1046):
+// the map closure, the reduceByKey shuffle and the reduce closure.  All device
+// memory is owned by the context and reused across calls (grow-only).
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fastkmer.h"
+#include "fk_internal.h"
+
+#define FK_EXPORT extern "C" __attribute__((visibility("default")))
+
+using namespace fk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            return set_err(e_ == hipErrorOutOfMemory ? FK_E_NOMEM : FK_E_DEVICE, "%s failed: %s (%s:%d)", \
+                           #expr, hipGetErrorString(e_), __FILE__, __LINE__);                        \
+    } while (0)
+
+#define FK_TRY(expr)             \
+    do {                         \
+        int r_ = (expr);         \
+        if (r_ != FK_OK) return r_; \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    template <typename T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+int ensure(DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return FK_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    const size_t want = bytes + bytes / 8 + 256;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(FK_E_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+    }
+    b.bytes = want;
+    return FK_OK;
+}
+
+void release(DevBuf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+int32_t clamp_bins(int32_t m, int32_t B) {
+    // test/package.scala:32: Math.min(Math.pow(4, m), max_b).toInt
+    double p = 1.0;
+    for (int i = 0; i < m; ++i) p *= 4.0;
+    const double b = p < (double)B ? p : (double)B;
+    return (int32_t)b;
+}
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+constexpr uint32_t CHUNK_RECORDS = 4096;  // records per expansion workgroup (never spans two bins)
+
+}  // namespace
+
+struct fk_ctx {
+    fk_config cfg{};
+    int32_t Bc = 0;    // b = min(4^m, B)
+    uint32_t G = 1;    // ranks
+    uint32_t nlb = 0;  // local bins: b = rank + G * lb
+    int W = 2, KW = 1;
+    FastMod fm{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS: route every bucket through 5b
+
+    // input
+    std::vector<uint8_t> host_in;
+    const uint8_t *d_fasta = nullptr;
+    uint64_t n_fasta = 0;
+    DevBuf fasta_own;
+
+    // parse + encode
+    DevBuf tile_last_nl, tile_prev_nl, tile_kept, tile_off, first_hdr, npos_dev, codes, valid;
+    // signature
+    DevBuf records, counters;
+    uint64_t nrec = 0, nkmers = 0;
+    bool mapped = false;
+    // destination partition (n_ranks > 1)
+    DevBuf dest_rec, dest_kmer, dest_off, dest_cursor;
+    std::vector<uint64_t> send_counts;
+    // reduce
+    DevBuf part_rec, part_kmer, part_off, part_cursor, precs, chunks, bin_chunk_begin;
+    DevBuf chunk_hist, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
+    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc;
+    DevBuf table_off, tkeys, tstate, tcounts;
+    ScanWorkspace ws;
+    // results
+    bool have_result = false;
+    uint64_t distinct = 0;
+    std::vector<uint64_t> h_bin_off;  // [nlb + 1]
+    fk_stats stats{};
+    // events: 0/1 parse, 2/3 signature, 4/5 partition, 6/7 count, 8/9 encode kernel, 10/11 sig kernel
+    hipEvent_t ev[12] = {};
+    bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
+};
+
+// ---------------------------------------------------------------------------
+// host-only helpers
+// ---------------------------------------------------------------------------
+
+FK_EXPORT int fk_abi_version(void) { return FK_ABI_VERSION; }
+
+FK_EXPORT const char *fk_last_error(void) { return g_err.c_str(); }
+
+FK_EXPORT int fk_config_init(fk_config *c) {
+    if (!c) return set_err(FK_E_INVALID, "null config");
+    // LocalTestKmerCounter.scala:20-33 defaults
+    c->k = 20;
+    c->m = 4;
+    c->x = 3;
+    c->B = 2000;
+    c->use_ht = 0;
+    c->sequence_type = 0;
+    c->write = 0;
+    c->n_ranks = 1;
+    c->rank = 0;
+    c->device = -1;
+    return FK_OK;
+}
+
+FK_EXPORT int32_t fk_clamped_bins(int32_t m, int32_t B) { return clamp_bins(m, B); }
+
+FK_EXPORT int fk_config_validate(const fk_config *c) {
+    if (!c) return set_err(FK_E_INVALID, "null config");
+    if (c->k < 1 || c->k > 64) return set_err(FK_E_INVALID, "k=%d out of range [1, 64]", c->k);
+    if (c->m < 1 || c->m > 15)
+        return set_err(FK_E_INVALID, "m=%d out of range [1, 15] (m >= 16 overflows Int shifts, SBKC:50)", c->m);
+    if (c->m > c->k) return set_err(FK_E_INVALID, "m=%d must not exceed k=%d", c->m, c->k);
+    if (c->B < 1) return set_err(FK_E_INVALID, "B=%d must be >= 1 (hash_to_bucket divides by B)", c->B);
+    if (c->use_ht != 0 && c->use_ht != 1) return set_err(FK_E_INVALID, "use_ht must be 0 or 1");
+    if (c->use_ht == 0 && c->x < 1)
+        return set_err(FK_E_INVALID,
+                       "x=%d: the sorted path needs x >= 1 (extractKXmers indexes R(runLength-1), SBKC:435/508)",
+                       c->x);
+    if (c->sequence_type != 0 && c->sequence_type != 1)
+        return set_err(FK_E_INVALID, "sequence_type must be 0 (short) or 1 (long)");
+    if (c->n_ranks < 1) return set_err(FK_E_INVALID, "n_ranks must be >= 1");
+    if (c->rank < 0 || c->rank >= c->n_ranks) return set_err(FK_E_INVALID, "rank %d out of [0, %d)", c->rank, c->n_ranks);
+    const int32_t bc = clamp_bins(c->m, c->B);
+    if ((uint32_t)bc > REC_BIN_MASK + 1u)
+        return set_err(FK_E_INVALID, "b = min(4^m, B) = %d exceeds the record header limit %u", bc, REC_BIN_MASK + 1u);
+    return FK_OK;
+}
+
+FK_EXPORT int fk_output_dir(const fk_config *c, const char *output_path, const char *prefix, char *out, size_t cap) {
+    if (!c || !out) return set_err(FK_E_INVALID, "null argument");
+    // test/package.scala:33 (debug == false)
+    const int n = snprintf(out, cap, "%s%sk%d_m%d_x%d_b%d_s%d", output_path ? output_path : "", prefix ? prefix : "",
+                           c->k, c->m, c->x, clamp_bins(c->m, c->B), c->sequence_type);
+    if (n < 0 || (size_t)n >= cap) return set_err(FK_E_RANGE, "output buffer too small (%d bytes needed)", n + 1);
+    return FK_OK;
+}
+
+FK_EXPORT size_t fk_record_bytes_for_k(int32_t k) { return k <= 32 ? 16 : 24; }
+
+FK_EXPORT uint64_t fk_synth_record_bytes(int32_t read_len) { return (uint64_t)read_len + 14; }
+
+static SynthParams make_synth(uint64_t first_read, uint64_t n_reads, int32_t read_len, uint64_t genome_len,
+                              uint64_t seed, double err_rate, double n_rate) {
+    SynthParams p;
+    p.first_read = first_read;
+    p.n_reads = n_reads;
+    p.genome_len = genome_len;
+    p.seed = seed;
+    p.read_len = (uint32_t)read_len;
+    p.rec_bytes = (uint32_t)read_len + 14;
+    const double two64 = 18446744073709551616.0;
+    p.err_thresh = (uint64_t)(err_rate * two64 * 0.999999);
+    p.n_thresh = (uint64_t)(n_rate * two64 * 0.999999);
+    return p;
+}
+
+FK_EXPORT int fk_synth_fasta_host(uint8_t *out, uint64_t first_read, uint64_t n_reads, int32_t read_len,
+                                  uint64_t genome_len, uint64_t seed, double err_rate, double n_rate) {
+    if (!out || read_len < 1 || genome_len < 1) return set_err(FK_E_INVALID, "bad synth arguments");
+    const SynthParams p = make_synth(first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate);
+    const uint64_t nb = n_reads * p.rec_bytes;
+    for (uint64_t i = 0; i < nb; ++i) out[i] = synth_byte(p, i);
+    return FK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+
+FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
+    if (!out) return set_err(FK_E_INVALID, "null output pointer");
+    *out = nullptr;
+    FK_TRY(fk_config_validate(cfg));
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return set_err(FK_E_DEVICE, "no HIP device available (%s): the k-mer counter runs on MI355X only",
+                       hipGetErrorString(e));
+    }
+    fk_ctx *c = new fk_ctx();
+    c->cfg = *cfg;
+    c->Bc = clamp_bins(cfg->m, cfg->B);
+    c->G = (uint32_t)cfg->n_ranks;
+    c->nlb = (uint32_t)((c->Bc - cfg->rank + (int)c->G - 1) / (int)c->G);
+    if (cfg->rank >= c->Bc) c->nlb = 0;
+    c->W = cfg->k <= 32 ? 2 : 3;
+    c->KW = cfg->k <= 32 ? 1 : 2;
+    c->fm = make_fastmod((uint32_t)c->Bc);
+    const char *dbg = getenv("FASTKMER_DEBUG_LARGE_BUCKETS");
+    c->force_large = dbg && dbg[0] == '1';
+    if (cfg->device >= 0) {
+        if (cfg->device >= ndev) {
+            delete c;
+            return set_err(FK_E_DEVICE, "device %d out of range (%d devices)", cfg->device, ndev);
+        }
+        e = hipSetDevice(cfg->device);
+        if (e != hipSuccess) {
+            delete c;
+            return set_err(FK_E_DEVICE, "hipSetDevice(%d): %s", cfg->device, hipGetErrorString(e));
+        }
+    }
+    (void)hipGetDevice(&c->device);
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return set_err(FK_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    c->own_stream = true;
+    for (auto &ev : c->ev) {
+        e = hipEventCreate(&ev);
+        if (e != hipSuccess) {
+            fk_destroy(c);
+            return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
+        }
+    }
+    *out = c;
+    return FK_OK;
+}
+
+FK_EXPORT void fk_destroy(fk_ctx *c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_prev_nl, &c->tile_kept, &c->tile_off,
+                      &c->first_hdr, &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters,
+                      &c->dest_rec, &c->dest_kmer, &c->dest_off, &c->dest_cursor, &c->part_rec, &c->part_kmer,
+                      &c->part_off, &c->part_cursor, &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_hist,
+                      &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
+                      &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
+                      &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
+                      &c->tcounts};
+    for (DevBuf *b : bufs) release(*b);
+    if (c->ws.ptr) (void)hipFree(c->ws.ptr);
+    for (auto &ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+FK_EXPORT int fk_set_stream(fk_ctx *c, void *s) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (c->own_stream && c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+    return FK_OK;
+}
+
+FK_EXPORT size_t fk_record_bytes(const fk_ctx *c) { return c ? (size_t)c->W * 8 : 0; }
+FK_EXPORT int32_t fk_num_bins(const fk_ctx *c) { return c ? c->Bc : 0; }
+
+static void reset_results(fk_ctx *c) {
+    c->mapped = false;
+    c->have_result = false;
+    c->distinct = 0;
+    c->h_bin_off.clear();
+}
+
+FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
+    (void)last;
+    if (!c || (!fasta && n)) return set_err(FK_E_INVALID, "null argument");
+    if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>())
+        return set_err(FK_E_STATE, "fk_ingest after fk_ingest_device on the same job");
+    c->host_in.insert(c->host_in.end(), fasta, fasta + n);
+    c->d_fasta = nullptr;
+    c->n_fasta = c->host_in.size();
+    reset_results(c);
+    return FK_OK;
+}
+
+FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
+    (void)last;
+    if (!c || (!d && n)) return set_err(FK_E_INVALID, "null argument");
+    c->host_in.clear();
+    reset_results(c);
+    if (((uintptr_t)d & 15) != 0) {
+        FK_TRY(ensure(c->fasta_own, n));
+        HIP_TRY(hipMemcpyAsync(c->fasta_own.p, d, n, hipMemcpyDeviceToDevice, c->stream));
+        c->d_fasta = c->fasta_own.as<uint8_t>();
+    } else {
+        c->d_fasta = (const uint8_t *)d;
+    }
+    c->n_fasta = n;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_reads, int32_t read_len,
+                                    uint64_t genome_len, uint64_t seed, double err_rate, double n_rate) {
+    if (!c || read_len < 1 || genome_len < 1) return set_err(FK_E_INVALID, "bad synth arguments");
+    const SynthParams p = make_synth(first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate);
+    const uint64_t nb = n_reads * p.rec_bytes;
+    FK_TRY(ensure(c->fasta_own, nb));
+    HIP_TRY(launch_synth(c->fasta_own.as<uint8_t>(), nb, p, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->host_in.clear();
+    c->d_fasta = c->fasta_own.as<uint8_t>();
+    c->n_fasta = nb;
+    reset_results(c);
+    return FK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// map side: parse + encode + signature + records (+ destination histogram)
+// ---------------------------------------------------------------------------
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0.f;
+    }
+    return ms;
+}
+
+FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    const double t_start = now_ms();
+    hipStream_t s = c->stream;
+    if (!c->host_in.empty() && !c->d_fasta) {
+        FK_TRY(ensure(c->fasta_own, c->host_in.size()));
+        HIP_TRY(hipMemcpyAsync(c->fasta_own.p, c->host_in.data(), c->host_in.size(), hipMemcpyHostToDevice, s));
+        c->d_fasta = c->fasta_own.as<uint8_t>();
+        c->n_fasta = c->host_in.size();
+    }
+    const uint64_t n = c->d_fasta ? c->n_fasta : 0;
+    reset_results(c);
+    c->stats = fk_stats{};
+    c->stats.fasta_bytes = n;
+    c->nrec = c->nkmers = 0;
+
+    const uint64_t ntiles = (n + ENC_TILE - 1) / ENC_TILE;
+    const uint64_t code_words = n / 16 + 2 * POS_PAD_WORDS + 512;
+    const uint64_t valid_words = n / 32 + 2 * POS_PAD_WORDS + 512;
+    FK_TRY(ensure(c->tile_last_nl, ntiles * 8));
+    FK_TRY(ensure(c->tile_prev_nl, ntiles * 8));
+    FK_TRY(ensure(c->tile_kept, ntiles * 8));
+    FK_TRY(ensure(c->tile_off, ntiles * 8));
+    FK_TRY(ensure(c->first_hdr, 8));
+    FK_TRY(ensure(c->npos_dev, 8));
+    FK_TRY(ensure(c->codes, code_words * 4));
+    FK_TRY(ensure(c->valid, valid_words * 4));
+    FK_TRY(ensure(c->counters, 64));
+
+    // 1. FASTA parse + 2-bit encode
+    HIP_TRY(hipEventRecord(c->ev[0], s));
+    HIP_TRY(launch_fill_u64(c->first_hdr.as<uint64_t>(), 1, (uint64_t)INT64_MAX, s));
+    HIP_TRY(hipMemsetAsync(c->codes.p, 0, code_words * 4, s));
+    HIP_TRY(hipMemsetAsync(c->valid.p, 0, valid_words * 4, s));
+    HIP_TRY(hipMemsetAsync(c->npos_dev.p, 0, 8, s));
+    if (n) {
+        HIP_TRY(launch_fasta_marks(c->d_fasta, n, c->tile_last_nl.as<int64_t>(),
+                                   c->first_hdr.as<unsigned long long>(), s));
+        HIP_TRY(scan_excl_max_i64(c->tile_last_nl.as<int64_t>(), c->tile_prev_nl.as<int64_t>(), ntiles, c->ws, s));
+        HIP_TRY(launch_fasta_count(c->d_fasta, n, c->tile_prev_nl.as<int64_t>(),
+                                   c->first_hdr.as<unsigned long long>(), c->tile_kept.as<uint64_t>(), s));
+        HIP_TRY(scan_excl_sum_u64(c->tile_kept.as<uint64_t>(), c->tile_off.as<uint64_t>(), ntiles,
+                                  c->npos_dev.as<uint64_t>(), c->ws, s));
+        HIP_TRY(hipEventRecord(c->ev[8], s));
+        HIP_TRY(launch_fasta_encode(c->d_fasta, n, c->tile_prev_nl.as<int64_t>(),
+                                    c->first_hdr.as<unsigned long long>(), c->tile_off.as<uint64_t>(),
+                                    c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), s));
+        HIP_TRY(hipEventRecord(c->ev[9], s));
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], s));
+
+    // 2. signature + super-k-mer records (retried once if the capacity estimate was short)
+    uint64_t rec_cap = std::max<uint64_t>(n / 6, 4096);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        FK_TRY(ensure(c->records, rec_cap * c->W * 8));
+        rec_cap = c->records.bytes / (c->W * 8);
+        HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
+        HIP_TRY(hipEventRecord(c->ev[2], s));
+        HIP_TRY(hipEventRecord(c->ev[10], s));
+        HIP_TRY(launch_superkmers(c->W, c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), n,
+                                  c->npos_dev.as<uint64_t>(), c->cfg.k, c->cfg.m, c->fm, c->records.as<uint64_t>(),
+                                  rec_cap, c->counters.as<unsigned long long>(), s));
+        HIP_TRY(hipEventRecord(c->ev[11], s));
+        HIP_TRY(hipEventRecord(c->ev[3], s));
+        uint64_t h[2];
+        HIP_TRY(hipMemcpyAsync(h, c->counters.p, 16, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->nrec = h[0];
+        c->nkmers = h[1];
+        if (c->nrec <= rec_cap) break;
+        rec_cap = c->nrec;
+    }
+    uint64_t npos = 0;
+    HIP_TRY(hipMemcpy(&npos, c->npos_dev.p, 8, hipMemcpyDeviceToHost));
+    c->stats.positions = npos;
+    c->stats.kmers = c->nkmers;
+    c->stats.superkmers = c->nrec;
+    c->stats.ms_parse = ev_ms(c->ev[0], c->ev[1]);
+    c->stats.ms_signature = ev_ms(c->ev[2], c->ev[3]);
+    c->stats.ms_encode_kernel = n ? ev_ms(c->ev[8], c->ev[9]) : 0.0;
+    c->stats.ms_signature_kernel = ev_ms(c->ev[10], c->ev[11]);
+
+    // 3a. destination histogram (records per rank)
+    c->send_counts.assign(c->G, 0);
+    if (c->G == 1) {
+        c->send_counts[0] = c->nrec;
+    } else if (c->nrec) {
+        FK_TRY(ensure(c->dest_rec, c->G * 8));
+        FK_TRY(ensure(c->dest_kmer, c->G * 8));
+        HIP_TRY(hipMemsetAsync(c->dest_rec.p, 0, c->G * 8, s));
+        HIP_TRY(hipMemsetAsync(c->dest_kmer.p, 0, c->G * 8, s));
+        HIP_TRY(launch_part_hist(c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, c->G,
+                                 c->dest_rec.as<uint64_t>(), c->dest_kmer.as<uint64_t>(), s));
+        HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest_rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (send_counts)
+        for (uint32_t r = 0; r < c->G; ++r) send_counts[r] = c->send_counts[r];
+    c->mapped = true;
+    c->stats.ms_total += now_ms() - t_start;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (!c->mapped) return set_err(FK_E_STATE, "fk_map_emit before fk_map");
+    if (cap_records < c->nrec) return set_err(FK_E_RANGE, "send buffer holds %llu records, need %llu",
+                                              (unsigned long long)cap_records, (unsigned long long)c->nrec);
+    if (!c->nrec) return FK_OK;
+    const double t0 = now_ms();
+    hipStream_t s = c->stream;
+    if (c->G == 1) {
+        HIP_TRY(hipMemcpyAsync(d_send, c->records.p, c->nrec * c->W * 8, hipMemcpyDeviceToDevice, s));
+    } else {
+        std::vector<uint64_t> off(c->G, 0);
+        for (uint32_t r = 1; r < c->G; ++r) off[r] = off[r - 1] + c->send_counts[r - 1];
+        FK_TRY(ensure(c->dest_off, c->G * 8));
+        FK_TRY(ensure(c->dest_cursor, c->G * 8));
+        HIP_TRY(hipMemcpyAsync(c->dest_off.p, off.data(), c->G * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(c->dest_cursor.p, 0, c->G * 8, s));
+        HIP_TRY(launch_part_scatter(c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, c->G,
+                                    c->dest_off.as<uint64_t>(), c->dest_cursor.as<unsigned long long>(),
+                                    (uint64_t *)d_send, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stats.ms_total += now_ms() - t0;
+    return FK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// reduce side
+// ---------------------------------------------------------------------------
+
+static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint64_t max_bin_kmers) {
+    hipStream_t s = c->stream;
+    const int k = c->cfg.k;
+    const uint32_t cap = (uint32_t)(SORT_CAP / c->KW);
+    // fine bits: ~8 cells per LDS bucket for the largest bin
+    int F = 1;
+    while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * (cap / 8) < max_bin_kmers) ++F;
+    F = std::min(F, 2 * k);
+    const uint64_t ncell_all = (uint64_t)c->nlb << F;
+    FK_TRY(ensure(c->chunk_hist, (uint64_t)nchunks * (4ull << F)));
+    FK_TRY(ensure(c->cell_total, ncell_all * 8));
+    FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
+    FK_TRY(ensure(c->flags, ncell_all * 4));
+    FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
+    FK_TRY(ensure(c->misc, 64));
+    HIP_TRY(launch_cell_hist(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+                             c->chunk_hist.as<uint32_t>(), s));
+    HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->chunk_hist.as<uint32_t>(),
+                               c->cell_total.as<uint64_t>(), s));
+    HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
+                              c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
+    const uint32_t small = cap / 4;
+    const uint32_t group = cap - cap / 4;
+    const uint32_t small_limit = c->force_large ? 0u : cap;
+    HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, small, group,
+                                c->flags.as<uint32_t>(), s));
+    HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), ncell_all,
+                                     c->flag_scan.as<uint64_t>() + ncell_all, c->ws, s));
+    uint64_t nbuckets = 0;
+    HIP_TRY(hipMemcpyAsync(&nbuckets, c->flag_scan.as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    FK_TRY(ensure(c->buckets, nbuckets * sizeof(Bucket)));
+    FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
+    FK_TRY(ensure(c->out_keys, total_kmers * 8 * c->KW));
+    FK_TRY(ensure(c->out_counts, total_kmers * 4));
+    FK_TRY(ensure(c->bucket_unique, (nbuckets + 1) * 8));
+    FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
+    HIP_TRY(launch_bucket_write(c->cell_base.as<uint64_t>(), c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(),
+                                c->nlb, F, total_kmers, c->buckets.as<Bucket>(), s));
+    HIP_TRY(launch_bucket_sizes(c->buckets.as<Bucket>(), nbuckets, total_kmers, s));
+    HIP_TRY(launch_cell_scatter(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+                                c->chunk_hist.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
+                                s));
+    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
+    HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+                               c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                               c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit, s));
+    uint64_t oversize = 0;
+    HIP_TRY(hipMemcpyAsync(&oversize, c->misc.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stats.oversize_buckets = oversize;
+    if (oversize)
+        HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+                                         c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                         c->bucket_unique.as<uint64_t>(), small_limit, s));
+    HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
+                              c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
+    uint64_t distinct = 0;
+    HIP_TRY(hipMemcpyAsync(&distinct, c->dense_off.as<uint64_t>() + nbuckets, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
+    FK_TRY(ensure(c->dense_counts, distinct * 4));
+    FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
+    HIP_TRY(launch_bucket_compact(c->KW, c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                  c->buckets.as<Bucket>(), nbuckets, c->dense_off.as<uint64_t>(),
+                                  c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(), s));
+    HIP_TRY(launch_bin_offsets(c->flag_scan.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
+                               c->bin_off.as<uint64_t>(), s));
+    c->distinct = distinct;
+    return FK_OK;
+}
+
+static int reduce_ht(fk_ctx *c, uint32_t nchunks, const std::vector<uint64_t> &bin_kmers) {
+    hipStream_t s = c->stream;
+    std::vector<uint64_t> toff(c->nlb + 1, 0);
+    for (uint32_t lb = 0; lb < c->nlb; ++lb) {
+        uint64_t cap = 16;
+        while (cap < 2 * bin_kmers[lb]) cap <<= 1;  // load factor <= 1/2 (upper bound of distinct)
+        toff[lb + 1] = toff[lb] + (bin_kmers[lb] ? cap : 0);
+    }
+    const uint64_t nslots = toff[c->nlb];
+    FK_TRY(ensure(c->table_off, ((uint64_t)c->nlb + 1) * 8));
+    FK_TRY(ensure(c->tkeys, nslots * 8 * c->KW));
+    FK_TRY(ensure(c->tcounts, nslots * 4));
+    FK_TRY(ensure(c->tstate, c->KW == 2 ? nslots * 4 : 16));
+    FK_TRY(ensure(c->flags, nslots * 4));
+    FK_TRY(ensure(c->flag_scan, (nslots + 1) * 8));
+    FK_TRY(ensure(c->misc, 64));
+    FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
+    HIP_TRY(hipMemcpyAsync(c->table_off.p, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c->tkeys.p, 0xff, nslots * 8 * c->KW, s));
+    HIP_TRY(hipMemsetAsync(c->tcounts.p, 0, nslots * 4, s));
+    if (c->KW == 2) HIP_TRY(hipMemsetAsync(c->tstate.p, 0, nslots * 4, s));
+    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
+    HIP_TRY(launch_ht_insert(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->cfg.k,
+                             c->table_off.as<uint64_t>(), c->tkeys.as<uint64_t>(), c->tstate.as<uint32_t>(),
+                             c->tcounts.as<uint32_t>(), c->misc.as<unsigned long long>(), s));
+    HIP_TRY(launch_ht_flags(c->tcounts.as<uint32_t>(), nslots, c->flags.as<uint32_t>(), s));
+    HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), nslots,
+                                     c->flag_scan.as<uint64_t>() + nslots, c->ws, s));
+    uint64_t h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&h[0], c->flag_scan.as<uint64_t>() + nslots, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&h[1], c->misc.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h[1]) return set_err(FK_E_DEVICE, "hash table overflow (%llu inserts failed)", (unsigned long long)h[1]);
+    const uint64_t distinct = h[0];
+    FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
+    FK_TRY(ensure(c->dense_counts, distinct * 4));
+    HIP_TRY(launch_ht_compact(c->KW, c->tkeys.as<uint64_t>(), c->tcounts.as<uint32_t>(), nslots,
+                              c->flag_scan.as<uint64_t>(), c->dense_keys.as<uint64_t>(),
+                              c->dense_counts.as<uint32_t>(), s));
+    HIP_TRY(launch_ht_bin_offsets(c->flag_scan.as<uint64_t>(), c->table_off.as<uint64_t>(), c->nlb, distinct,
+                                  c->bin_off.as<uint64_t>(), s));
+    c->distinct = distinct;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
+    const double t0 = now_ms();
+    hipStream_t s = c->stream;
+    c->have_result = false;
+    const uint32_t nlb = c->nlb;
+    FK_TRY(ensure(c->part_rec, ((uint64_t)nlb + 1) * 8));
+    FK_TRY(ensure(c->part_kmer, ((uint64_t)nlb + 1) * 8));
+    FK_TRY(ensure(c->part_off, ((uint64_t)nlb + 1) * 8));
+    FK_TRY(ensure(c->part_cursor, ((uint64_t)nlb + 1) * 8));
+    HIP_TRY(hipEventRecord(c->ev[4], s));
+    HIP_TRY(hipMemsetAsync(c->part_rec.p, 0, ((uint64_t)nlb + 1) * 8, s));
+    HIP_TRY(hipMemsetAsync(c->part_kmer.p, 0, ((uint64_t)nlb + 1) * 8, s));
+    HIP_TRY(launch_part_hist(c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, nlb, c->part_rec.as<uint64_t>(),
+                             c->part_kmer.as<uint64_t>(), s));
+    std::vector<uint64_t> brec(nlb), bkm(nlb);
+    if (nlb) {
+        HIP_TRY(hipMemcpyAsync(brec.data(), c->part_rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(bkm.data(), c->part_kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    // record offsets per local bin and chunk table (chunks never span bins)
+    std::vector<uint64_t> roff(nlb + 1, 0);
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb(nlb + 1, 0);
+    uint64_t total_kmers = 0, max_bin = 0;
+    for (uint32_t lb = 0; lb < nlb; ++lb) {
+        roff[lb + 1] = roff[lb] + brec[lb];
+        total_kmers += bkm[lb];
+        max_bin = std::max(max_bin, bkm[lb]);
+        bcb[lb] = (uint32_t)chunks.size();
+        for (uint64_t r = roff[lb]; r < roff[lb + 1]; r += CHUNK_RECORDS) {
+            Chunk ch;
+            ch.rec_begin = r;
+            ch.rec_end = std::min<uint64_t>(r + CHUNK_RECORDS, roff[lb + 1]);
+            ch.lbin = lb;
+            ch.pad = 0;
+            chunks.push_back(ch);
+        }
+    }
+    bcb[nlb] = (uint32_t)chunks.size();
+    const uint32_t nchunks = (uint32_t)chunks.size();
+    if (roff[nlb] != nrecv)
+        return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
+                       (unsigned long long)roff[nlb], (unsigned long long)nrecv);
+    FK_TRY(ensure(c->precs, nrecv * c->W * 8));
+    FK_TRY(ensure(c->chunks, nchunks * sizeof(Chunk)));
+    FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)nlb + 1) * 4));
+    HIP_TRY(hipMemcpyAsync(c->part_off.p, roff.data(), (nlb + 1) * 8, hipMemcpyHostToDevice, s));
+    if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), (nlb + 1) * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c->part_cursor.p, 0, ((uint64_t)nlb + 1) * 8, s));
+    HIP_TRY(launch_part_scatter(c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, nlb, c->part_off.as<uint64_t>(),
+                                c->part_cursor.as<unsigned long long>(), c->precs.as<uint64_t>(), s));
+    HIP_TRY(hipEventRecord(c->ev[5], s));
+    HIP_TRY(hipEventRecord(c->ev[6], s));
+    if (c->cfg.use_ht)
+        FK_TRY(reduce_ht(c, nchunks, bkm));
+    else
+        FK_TRY(reduce_sorted(c, nchunks, total_kmers, max_bin));
+    HIP_TRY(hipEventRecord(c->ev[7], s));
+    c->h_bin_off.assign((size_t)nlb + 1, 0);
+    HIP_TRY(hipMemcpyAsync(c->h_bin_off.data(), c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stats.records_received = nrecv;
+    c->stats.distinct = c->distinct;
+    c->stats.ms_partition = ev_ms(c->ev[4], c->ev[5]);
+    c->stats.ms_count = ev_ms(c->ev[6], c->ev[7]);
+    c->stats.ms_total += now_ms() - t0;
+    c->have_result = true;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_finish(fk_ctx *c) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (c->G != 1) return set_err(FK_E_STATE, "fk_finish is the single-rank path; use fk_map/fk_map_emit/fk_reduce");
+    FK_TRY(fk_map(c, nullptr));
+    return fk_reduce(c, c->records.p, c->nrec);
+}
+
+// ---------------------------------------------------------------------------
+// results
+// ---------------------------------------------------------------------------
+
+static bool owns(const fk_ctx *c, int32_t b) { return b >= 0 && b < c->Bc && (uint32_t)b % c->G == (uint32_t)c->cfg.rank; }
+
+FK_EXPORT int fk_bin_sizes(fk_ctx *c, uint64_t *out) {
+    if (!c || !out) return set_err(FK_E_INVALID, "null argument");
+    if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
+    for (int32_t b = 0; b < c->Bc; ++b) {
+        if (owns(c, b)) {
+            const uint32_t lb = (uint32_t)b / c->G;
+            out[b] = c->h_bin_off[lb + 1] - c->h_bin_off[lb];
+        } else {
+            out[b] = 0;
+        }
+    }
+    return FK_OK;
+}
+
+FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *counts, size_t cap, size_t *n) {
+    if (!c || !n) return set_err(FK_E_INVALID, "null argument");
+    if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
+    if (bin < 0 || bin >= c->Bc) return set_err(FK_E_RANGE, "bin %d out of [0, %d)", bin, c->Bc);
+    if (!owns(c, bin)) {
+        *n = 0;
+        return FK_OK;
+    }
+    const uint32_t lb = (uint32_t)bin / c->G;
+    const uint64_t b0 = c->h_bin_off[lb], cnt = c->h_bin_off[lb + 1] - b0;
+    *n = (size_t)cnt;
+    if (cnt == 0) return FK_OK;
+    if (cap < cnt) return set_err(FK_E_RANGE, "bin %d has %llu k-mers, buffer holds %zu", bin, (unsigned long long)cnt, cap);
+    if (keys)
+        HIP_TRY(hipMemcpy(keys, c->dense_keys.as<uint64_t>() + b0 * c->KW, cnt * 8 * c->KW, hipMemcpyDeviceToHost));
+    if (counts) HIP_TRY(hipMemcpy(counts, c->dense_counts.as<uint32_t>() + b0, cnt * 4, hipMemcpyDeviceToHost));
+    return FK_OK;
+}
+
+FK_EXPORT int fk_get_stats(fk_ctx *c, fk_stats *out) {
+    if (!c || !out) return set_err(FK_E_INVALID, "null argument");
+    *out = c->stats;
+    return FK_OK;
+}
+
+static int mkdir_p(const std::string &path) {
+    std::string cur;
+    for (size_t i = 0; i < path.size(); ++i) {
+        cur.push_back(path[i]);
+        if ((path[i] == '/' && i > 0) || i + 1 == path.size()) {
+            if (mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return -1;
+        }
+    }
+    return 0;
+}
+
+// Kmer.toString (package.scala:416-454, 496-500) + "\t" + count + "\n"
+static size_t format_line(char *dst, uint64_t hi, uint64_t lo, uint32_t cnt, int k) {
+    static const char rep[4] = {'A', 'C', 'G', 'T'};
+    for (int t = 0; t < k; ++t) {
+        const int bit = 2 * (k - 1 - t);
+        const uint64_t v = bit >= 64 ? (hi >> (bit - 64)) : (lo >> bit);
+        dst[t] = rep[v & 3];
+    }
+    size_t p = (size_t)k;
+    dst[p++] = '\t';
+    char tmp[16];
+    int q = 0;
+    do {
+        tmp[q++] = (char)('0' + cnt % 10);
+        cnt /= 10;
+    } while (cnt);
+    while (q) dst[p++] = tmp[--q];
+    dst[p++] = '\n';
+    return p;
+}
+
+FK_EXPORT int fk_write_bins(fk_ctx *c, const char *out_dir) {
+    if (!c || !out_dir) return set_err(FK_E_INVALID, "null argument");
+    if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
+    if (mkdir_p(out_dir) != 0) return set_err(FK_E_IO, "cannot create %s: %s", out_dir, strerror(errno));
+    const uint64_t D = c->distinct;
+    std::vector<uint64_t> hk(D * c->KW);
+    std::vector<uint32_t> hc(D);
+    if (D) {
+        HIP_TRY(hipMemcpy(hk.data(), c->dense_keys.p, D * 8 * c->KW, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(hc.data(), c->dense_counts.p, D * 4, hipMemcpyDeviceToHost));
+    }
+    const int k = c->cfg.k;
+    const int KW = c->KW;
+    const bool eof = c->cfg.use_ht == 0;
+    const std::string dir(out_dir);
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<int> errs(nth, 0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; ++t) {
+        th.emplace_back([&, t]() {
+            std::vector<char> buf;
+            for (uint32_t lb = t; lb < c->nlb; lb += nth) {
+                const uint64_t b0 = c->h_bin_off[lb], b1 = c->h_bin_off[lb + 1];
+                if (b1 == b0) continue;
+                const uint32_t bin = (uint32_t)c->cfg.rank + lb * c->G;
+                buf.resize((b1 - b0) * (size_t)(k + 13) + 8);
+                size_t p = 0;
+                for (uint64_t i = b0; i < b1; ++i) {
+                    const uint64_t hi = KW == 2 ? hk[2 * i] : 0, lo = KW == 2 ? hk[2 * i + 1] : hk[i];
+                    p += format_line(buf.data() + p, hi, lo, hc[i], k);
+                }
+                if (eof) {
+                    memcpy(buf.data() + p, "EOF", 3);
+                    p += 3;
+                }
+                const std::string path = dir + "/bin" + std::to_string(bin);
+                FILE *f = fopen(path.c_str(), "wb");
+                if (!f || fwrite(buf.data(), 1, p, f) != p) errs[t] = 1;
+                if (f) fclose(f);
+            }
+        });
+    }
+    for (auto &x : th) x.join();
+    for (int e : errs)
+        if (e) return set_err(FK_E_IO, "writing bin files under %s failed", out_dir);
+    return FK_OK;
+}

@@ -1,0 +1,116 @@
+// fk_internal.h -- device pipeline stages (launch wrappers in fk_kernels.hip).
+//
+// Data layout in HBM (one rank):
+//   fasta      u8[n]                     input bytes (owned or borrowed)
+//   codes      u32[npos/16 + pad]        2-bit bases, 16 per word, MSB-first
+//   valid      u32[npos/32 + pad]        1 bit per position (1 = A/C/G/T)
+//   records    u64[W * nrec]             super-k-mer records, W = 2 (k<=32) or 3
+//   keys       u64[KW * nkmers]          canonical k-mers scattered by (bin, cell)
+//   out_keys   u64[KW * nkmers]          per-bucket sorted unique keys
+//   dense      u64[KW * distinct] + u32 counts, bin_off[nbins_local + 1]
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fk_common.h"
+
+namespace fk {
+
+constexpr int ENC_TILE = 16384;  // FASTA bytes per parse/encode workgroup
+constexpr int SIG_TILE = 4096;   // k-mer start positions per signature workgroup (256 x 16)
+constexpr int SIG_PPT = 16;      // positions per thread == max k-mers per record
+constexpr int POS_PAD_WORDS = 64;  // zero words after the packed stream (halo reads)
+constexpr int SORT_CAP = 4096;   // keys per LDS-sorted bucket (u64 keys; half for 128-bit keys)
+constexpr int MAX_FINE_BITS = 13;
+
+// record header (low 32 bits of word 0): bin | (n-1) << 22
+constexpr int REC_BIN_BITS = 22;
+constexpr uint32_t REC_BIN_MASK = (1u << REC_BIN_BITS) - 1u;
+
+struct Bucket {
+    uint64_t begin;  // first key index (into keys / out_keys)
+    uint32_t n;      // keys in the bucket
+    uint32_t lbin;   // local bin
+};
+
+struct Chunk {
+    uint64_t rec_begin, rec_end;  // records [begin, end) of one local bin
+    uint32_t lbin, pad;
+};
+
+// Grow-only scratch space for the scans.
+struct ScanWorkspace {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+// ---- scans (exclusive); `total` (device, may be null) receives the sum/max
+hipError_t scan_excl_sum_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total, ScanWorkspace &ws,
+                             hipStream_t s);
+hipError_t scan_excl_sum_u32_to_u64(const uint32_t *in, uint64_t *out, uint64_t n, uint64_t *total,
+                                    ScanWorkspace &ws, hipStream_t s);
+hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWorkspace &ws, hipStream_t s);
+
+// ---- FASTA parse + encode (records -> compacted packed positions)
+hipError_t launch_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl, unsigned long long *first_hdr,
+                              hipStream_t s);
+hipError_t launch_fasta_count(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
+                              const unsigned long long *first_hdr, uint64_t *tile_kept, hipStream_t s);
+hipError_t launch_fasta_encode(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
+                               const unsigned long long *first_hdr, const uint64_t *tile_off, uint32_t *codes,
+                               uint32_t *valid, hipStream_t s);
+
+// ---- signature + super-k-mer records
+hipError_t launch_superkmers(int W, const uint32_t *codes, const uint32_t *valid, uint64_t npos_bound,
+                             const uint64_t *npos_dev, int k, int m, FastMod fm, uint64_t *records, uint64_t rec_cap,
+                             unsigned long long *counters, hipStream_t s);
+hipError_t launch_fill_u64(uint64_t *p, uint64_t n, uint64_t v, hipStream_t s);
+
+// ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]
+hipError_t launch_part_hist(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
+                            uint64_t *part_rec, uint64_t *part_kmer, hipStream_t s);
+hipError_t launch_part_scatter(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
+                               const uint64_t *part_off, unsigned long long *part_cursor, uint64_t *out,
+                               hipStream_t s);
+
+// ---- sorted count
+hipError_t launch_cell_hist(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,
+                            int F, uint32_t *chunk_hist, hipStream_t s);
+hipError_t launch_cell_prefix(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, uint32_t *chunk_hist,
+                              uint64_t *cell_total, hipStream_t s);
+hipError_t launch_bucket_flags(const uint64_t *cell_base, const uint64_t *cell_total, uint32_t nlbins, int F,
+                               uint32_t small_cap, uint32_t group, uint32_t *flags, hipStream_t s);
+hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags, const uint64_t *flag_scan,
+                               uint32_t nlbins, int F, uint64_t total_keys, Bucket *buckets, hipStream_t s);
+hipError_t launch_cell_scatter(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,
+                               int F, const uint32_t *chunk_hist, const uint64_t *cell_base, uint64_t *keys,
+                               hipStream_t s);
+hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
+                              uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+                              unsigned long long *oversize, uint32_t small_limit, hipStream_t s);
+hipError_t launch_bucket_sort_large(int KW, uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
+                                    uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+                                    uint32_t small_limit, hipStream_t s);
+hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_t *out_counts,
+                                 const Bucket *buckets, uint64_t nbuckets, const uint64_t *dense_off,
+                                 uint64_t *dense_keys, uint32_t *dense_counts, hipStream_t s);
+hipError_t launch_bin_offsets(const uint64_t *flag_scan, const uint64_t *dense_off, uint32_t nlbins, int F,
+                              uint64_t nbuckets, uint64_t *bin_off, hipStream_t s);
+hipError_t launch_bucket_sizes(Bucket *buckets, uint64_t nb, uint64_t total_keys, hipStream_t s);
+
+// ---- hash count (extractKXmersHT)
+hipError_t launch_ht_insert(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,
+                            const uint64_t *table_off, uint64_t *tkeys, uint32_t *tstate, uint32_t *tcounts,
+                            unsigned long long *fail, hipStream_t s);
+hipError_t launch_ht_flags(const uint32_t *tcounts, uint64_t nslots, uint32_t *flags, hipStream_t s);
+hipError_t launch_ht_compact(int KW, const uint64_t *tkeys, const uint32_t *tcounts, uint64_t nslots,
+                             const uint64_t *slot_scan, uint64_t *dense_keys, uint32_t *dense_counts,
+                             hipStream_t s);
+hipError_t launch_ht_bin_offsets(const uint64_t *slot_scan, const uint64_t *table_off, uint32_t nlbins,
+                                 uint64_t total, uint64_t *bin_off, hipStream_t s);
+
+// ---- synthetic input
+hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);
+
+}  // namespace fk

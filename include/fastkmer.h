@@ -1,0 +1,140 @@
+/*
+ * fastkmer.h -- C-ABI of the MI355X-native exact k-mer counter.
+ *
+ * Drop-in boundary for the hot path of maruscia/fastkmer: the body of
+ *   SparkBinKmerCounter.executeJob(spark, configuration)
+ *     src/main/scala/skc/SparkBinKmerCounter.scala:989-1046
+ * i.e. the map closure getSuperKmers / getSuperKmersWithBinSizes (:34-169,
+ * :290-426), the signature->bin shuffle reduceByKey (:1035, :1042) and the
+ * reduce closures extractKXmers / extractKXmersHT (:428-660, :664-739).
+ * INTEGRATION.md shows the JNI binding a Scala maintainer would add and the
+ * ctypes binding used by this repository's tests.
+ *
+ * Plain C types only.  Every call returns FK_OK (0) or a negative FK_E_*
+ * code and never aborts; fk_last_error() returns a thread-local message.
+ * A context is used by one host thread at a time.  All GPU work runs on the
+ * context's HIP stream on the device selected by fk_config.device.
+ */
+#ifndef FASTKMER_H
+#define FASTKMER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FK_ABI_VERSION 1
+
+#define FK_OK 0
+#define FK_E_INVALID (-1) /* bad argument or configuration (reference: require / AIOOBE) */
+#define FK_E_STATE (-2)   /* call out of order (e.g. fk_get_bin before fk_finish) */
+#define FK_E_DEVICE (-3)  /* HIP runtime failure or no usable GPU */
+#define FK_E_NOMEM (-4)   /* device or host allocation failed */
+#define FK_E_IO (-5)      /* file system error while writing bins */
+#define FK_E_RANGE (-6)   /* caller buffer too small / bin out of range */
+
+/* Mirrors skc.test.testutil.TestConfiguration (test/package.scala:16-42). */
+typedef struct fk_config {
+    int32_t k;             /* k-mer length, 1..64 (reference: any; Kmer packs 31 nt/Long) */
+    int32_t m;             /* signature length, 1..15 (m >= 16 breaks Int shifts, SBKC:50) */
+    int32_t x;             /* (k,x)-mer factor; must be >= 1 when use_ht == 0 (SBKC:435) */
+    int32_t B;             /* requested bins; the library uses b = min(4^m, B) (package.scala:32) */
+    int32_t use_ht;        /* 0: sorted count (extractKXmers), 1: hash count (extractKXmersHT) */
+    int32_t sequence_type; /* 0: FASTA short reads, 1: long sequence (FASTdoop long format) */
+    int32_t write;         /* reference "write" flag; only consulted by the CLI */
+    int32_t n_ranks;       /* >= 1: bins are owned round-robin, bin % n_ranks == rank */
+    int32_t rank;          /* 0..n_ranks-1 */
+    int32_t device;        /* HIP device ordinal, -1 = current device */
+} fk_config;
+
+typedef struct fk_ctx fk_ctx;
+
+/* Per-context statistics (device times are HIP-event times on the ctx stream). */
+typedef struct fk_stats {
+    uint64_t fasta_bytes;      /* bytes ingested */
+    uint64_t positions;        /* sequence positions after FASTA parsing */
+    uint64_t bases;            /* A/C/G/T/N... sequence bytes (input bases) */
+    uint64_t kmers;            /* valid k-mer windows counted */
+    uint64_t superkmers;       /* super-k-mer records produced by fk_map */
+    uint64_t records_received; /* records counted by fk_reduce */
+    uint64_t distinct;         /* distinct canonical k-mers owned by this rank */
+    uint64_t oversize_buckets; /* buckets that took the large-bucket path */
+    double ms_parse;           /* FASTA parse + 2-bit encode kernels */
+    double ms_signature;       /* signature / super-k-mer kernel */
+    double ms_partition;       /* record partition kernels */
+    double ms_count;           /* expand + bucket + sort/hash + compact kernels */
+    double ms_total;           /* fk_map + fk_reduce wall time on the host */
+    double ms_encode_kernel;   /* last launch of the encode kernel */
+    double ms_signature_kernel;/* last launch of the signature kernel */
+} fk_stats;
+
+/* ---- host-only helpers (no GPU needed) ---------------------------------- */
+
+int fk_abi_version(void);
+/* Defaults of LocalTestKmerCounter.main (LocalTestKmerCounter.scala:20-33). */
+int fk_config_init(fk_config *cfg);
+/* Validates without touching the GPU; FK_E_INVALID with a message on error. */
+int fk_config_validate(const fk_config *cfg);
+/* b = min(4^m, B) exactly as TestConfiguration.b (test/package.scala:32). */
+int32_t fk_clamped_bins(int32_t m, int32_t B);
+/* TestConfiguration.outputDir (test/package.scala:33, debug == false). */
+int fk_output_dir(const fk_config *cfg, const char *output_path, const char *prefix, char *out, size_t cap);
+/* Bytes of one packed super-k-mer record for k (16 for k <= 32, 24 for k <= 64). */
+size_t fk_record_bytes_for_k(int32_t k);
+/* Deterministic synthetic short-read FASTA (">r%010d\n" + read + "\n"),
+ * identical on host and device; see fk_synth_fasta_device. */
+uint64_t fk_synth_record_bytes(int32_t read_len);
+int fk_synth_fasta_host(uint8_t *out, uint64_t first_read, uint64_t n_reads, int32_t read_len,
+                        uint64_t genome_len, uint64_t seed, double err_rate, double n_rate);
+
+/* ---- context ------------------------------------------------------------ */
+
+int fk_create(const fk_config *cfg, fk_ctx **out);
+void fk_destroy(fk_ctx *ctx);
+const char *fk_last_error(void);
+/* Optional: run on a caller-owned hipStream_t (e.g. torch's current stream). */
+int fk_set_stream(fk_ctx *ctx, void *hip_stream);
+
+/* Input.  fk_ingest copies host FASTA bytes to the device (may be called
+ * repeatedly: the chunks are concatenated).  fk_ingest_device borrows a
+ * device buffer (zero-copy; it must stay valid until fk_map returns). */
+int fk_ingest(fk_ctx *ctx, const uint8_t *fasta, size_t n, int last);
+int fk_ingest_device(fk_ctx *ctx, const void *d_fasta, size_t n, int last);
+/* Fill the device input with fk_synth_fasta-compatible data (benchmarks). */
+int fk_synth_fasta_device(fk_ctx *ctx, uint64_t first_read, uint64_t n_reads, int32_t read_len,
+                          uint64_t genome_len, uint64_t seed, double err_rate, double n_rate);
+
+/* Map side (getSuperKmers, SBKC:34-169): parse, encode, signature,
+ * super-k-mer records; send_counts[r] = records destined to rank r. */
+int fk_map(fk_ctx *ctx, uint64_t *send_counts);
+size_t fk_record_bytes(const fk_ctx *ctx);
+/* Write the mapped records into d_send grouped by destination rank
+ * (rank 0 first), send_counts as returned by fk_map. */
+int fk_map_emit(fk_ctx *ctx, void *d_send, uint64_t cap_records);
+/* Reduce side (reduceByKey + extractKXmers[HT]): count the records in
+ * d_recv (device memory, fk_record_bytes each, all owned by this rank). */
+int fk_reduce(fk_ctx *ctx, const void *d_recv, uint64_t n_records);
+/* Single rank: fk_map + fk_reduce on the local records. */
+int fk_finish(fk_ctx *ctx);
+
+/* ---- results (device resident; copied out on request) ------------------ */
+
+int32_t fk_num_bins(const fk_ctx *ctx); /* b = min(4^m, B) */
+/* distinct[b] for all b (0 for bins owned by other ranks). */
+int fk_bin_sizes(fk_ctx *ctx, uint64_t *distinct_per_bin);
+/* Canonical k-mers of bin b and their counts.  useHT=0: ascending
+ * lexicographic order (extractKXmers); useHT=1: table order.  keys hold one
+ * word per k-mer for k <= 32 and two (first k-32 bases, last 32 bases) for
+ * k > 32, 2 bits per base, A=0 C=1 G=2 T=3, most significant base first. */
+int fk_get_bin(fk_ctx *ctx, int32_t bin, uint64_t *keys, uint32_t *counts, size_t cap, size_t *n);
+/* Reference byte format: <out_dir>/bin<b>, "<kmer>\t<count>\n" lines, plus
+ * "EOF" (no newline) when use_ht == 0 (SBKC:550-606, :715-734). */
+int fk_write_bins(fk_ctx *ctx, const char *out_dir);
+int fk_get_stats(fk_ctx *ctx, fk_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FASTKMER_H */

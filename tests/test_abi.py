@@ -1,0 +1,114 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+symbol include/fastkmer.h declares, validates configurations like the
+reference (and fails loudly when no GPU is present), and the host helpers
+mirror TestConfiguration / LocalTestKmerCounter."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import fastkmer_amd as fk
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    from fastkmer_amd import build
+    build.build()
+
+
+def test_exports_every_header_symbol():
+    names = fk.header_functions()
+    assert len(names) >= 20
+    L = ctypes.CDLL(fk.LIB_PATH)
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    out = subprocess.check_output(["nm", "-D", "--defined-only", fk.LIB_PATH]).decode()
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(names) <= exported
+    # nothing but the C-ABI leaks out of the shared object
+    assert {n for n in exported if not n.startswith("fk_")} <= {"_init", "_fini"}
+
+
+def test_abi_version():
+    assert fk.lib().fk_abi_version() == 1
+
+
+@pytest.mark.parametrize("kw,ok", [
+    (dict(k=28, m=10, x=3, B=2048), True),
+    (dict(k=55, m=12, x=3, B=8192), True),
+    (dict(k=64, m=15, x=1, B=1), True),
+    (dict(k=28, m=10, x=0, B=2048), False),            # extractKXmers AIOOBE (SBKC:508)
+    (dict(k=28, m=10, x=0, B=2048, use_ht=True), True),  # HT path never reads x
+    (dict(k=28, m=16, x=3, B=2048), False),            # Int shift overflow (SBKC:50)
+    (dict(k=65, m=10, x=3, B=2048), False),
+    (dict(k=9, m=10, x=3, B=2048), False),
+    (dict(k=28, m=10, x=3, B=0), False),
+    (dict(k=28, m=10, x=3, B=2048, sequence_type=2), False),
+    (dict(k=28, m=10, x=3, B=2048, n_ranks=2, rank=2), False),
+    (dict(k=28, m=12, x=3, B=1 << 23), False),         # record header holds 22 bits of bin
+])
+def test_config_validation(kw, ok):
+    if ok:
+        fk.validate(**kw)
+    else:
+        with pytest.raises(fk.FastKmerError) as e:
+            fk.validate(**kw)
+        assert e.value.code == -1
+
+
+def test_clamped_bins_and_output_dir():
+    assert fk.clamped_bins(10, 2048) == 2048
+    assert fk.clamped_bins(3, 2048) == 64
+    assert fk.clamped_bins(15, 2**31 - 1) == 4**15
+    c = fk.make_config(28, 10, 3, 2048)
+    buf = ctypes.create_string_buffer(512)
+    assert fk.lib().fk_output_dir(ctypes.byref(c), b"/out/", b"gallus", buf, 512) == 0
+    tc = fk.TestConfiguration("in.fa", "/out/", 28, 10, 3, max_b=2048, prefix="gallus")
+    assert buf.value.decode() == tc.outputDir == "/out/galluskk28_m10_x3_b2048_s0".replace("kk", "k")
+    assert fk.TestConfiguration("a", "/o/", 21, 3, 2, max_b=2048).b == 64
+    assert fk.TestConfiguration("a", "/o/", 21, 3, 2, debug=True).outputDir == "/tmp/k21_m3_x2_b64"
+
+
+def test_record_bytes():
+    assert fk.record_bytes_for_k(28) == 16
+    assert fk.record_bytes_for_k(32) == 16
+    assert fk.record_bytes_for_k(33) == 24
+    assert fk.record_bytes_for_k(55) == 24
+
+
+def test_synth_fasta_format_and_determinism():
+    a = fk.synth_fasta(50, 100, 10_000, seed=7)
+    b = fk.synth_fasta(50, 100, 10_000, seed=7)
+    assert a == b and len(a) == 50 * 114
+    recs = a.split(b"\n")
+    assert recs[0] == b">r0000000000" and recs[2] == b">r0000000001"
+    assert all(len(recs[i]) == 100 for i in range(1, 100, 2))
+    assert set(b"".join(recs[1::2])) <= set(b"ACGTN")
+    # a shard starting at read 20 is the tail of the full file
+    assert fk.synth_fasta(30, 100, 10_000, seed=7, first_read=20) == a[20 * 114:]
+    # error-free reads come from the virtual genome: every read is a substring
+    # of it or of its reverse complement, so k-mers repeat across reads
+    clean = fk.synth_fasta(400, 100, 2_000, seed=3, err_rate=0.0, n_rate=0.0)
+    import collections
+    reads = clean.split(b"\n")[1::2]
+    kmers = collections.Counter(r[i:i + 21] for r in reads for i in range(80))
+    assert max(kmers.values()) > 3
+
+
+def test_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(fk.FastKmerError) as e:
+        fk.KmerCounter(28, 10)
+    assert e.value.code == -3 and "no HIP device" in str(e.value)
+
+
+def test_cli_usage_errors():
+    fk_cli = fk.CLI_PATH
+    r = subprocess.run([fk_cli], capture_output=True)
+    assert r.returncode == 2 and b"usage" in r.stderr
+    r = subprocess.run([fk_cli, "28", "16", "3", "2048", "0", "0", "in", "out", "p", "0", "0", "0"],
+                       capture_output=True)
+    assert r.returncode == 1 and b"invalid configuration" in r.stderr

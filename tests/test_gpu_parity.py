@@ -1,0 +1,288 @@
+"""HIP path vs the CPU oracle, through the C-ABI (needs an MI355X).
+
+Bit-exact: every bin's (canonical k-mer, count) list must equal the
+oracle's, in the same (ascending) order for useHT=0 and as a set for
+useHT=1, and written bin files must be byte-identical to the reference
+format.  Golden fixtures (tests/golden) pin the small cases; seeded synthetic
+inputs cover the BASELINE configurations at sizes the oracle finishes in
+seconds; size-independent properties cover the full 1 GB configuration.
+"""
+import json
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import fastkmer_amd as fk
+import oracle
+from conftest import GOLDEN, golden_cases
+
+pytestmark = pytest.mark.gpu
+
+
+def counter_arrays(kc, b):
+    keys, counts = kc.get_bin(b)
+    if kc.k > 32:
+        keys = keys.reshape(-1, 2)
+        return keys[:, 0].copy(), keys[:, 1].copy(), counts
+    return np.zeros(len(keys), dtype=np.uint64), keys, counts
+
+
+def assert_same_as_oracle(kc, ref, ordered=True):
+    sizes = kc.bin_sizes()
+    assert len(sizes) == ref.nbins
+    ref_sizes = ref.bin_sizes()
+    bad = np.nonzero(sizes.astype(np.int64) != ref_sizes)[0]
+    assert len(bad) == 0, f"bin sizes differ in {len(bad)} bins, e.g. bin {bad[:5]}"
+    for b in np.nonzero(ref_sizes)[0].tolist():
+        hi, lo, cnt = counter_arrays(kc, b)
+        rhi, rlo, rcnt = ref.bin_arrays(b)
+        if not ordered:
+            order = np.lexsort((lo, hi))
+            hi, lo, cnt = hi[order], lo[order], cnt[order]
+        assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo), f"keys differ in bin {b}"
+        assert np.array_equal(cnt, rcnt), f"counts differ in bin {b}"
+
+
+def run_counter(fasta, k, m, x=3, B=2048, use_ht=False, sequence_type=0):
+    kc = fk.KmerCounter(k, m, x, B, use_ht, sequence_type)
+    kc.ingest(fasta)
+    kc.finish()
+    return kc
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name + ".fa"), "rb") as f:
+        fasta = f.read()
+    with open(os.path.join(GOLDEN, name + ".expected.json")) as f:
+        expected = json.load(f)
+    return fasta, expected
+
+
+@pytest.mark.parametrize("name", sorted(golden_cases()))
+def test_golden_sorted(name):
+    p = golden_cases()[name]
+    fasta, expected = load_golden(name)
+    kc = run_counter(fasta, p["k"], p["m"], p["x"], p["B"], False, p.get("sequence_type", 0))
+    sizes = kc.bin_sizes()
+    got = {f"bin{b}": kc.bin_text(b) for b in np.nonzero(sizes)[0].tolist()}
+    assert got == expected
+    assert kc.stats()["kmers"] == p["total_kmers"]
+
+
+@pytest.mark.parametrize("name", sorted(golden_cases()))
+def test_golden_hash(name):
+    p = golden_cases()[name]
+    fasta, expected = load_golden(name)
+    kc = run_counter(fasta, p["k"], p["m"], p["x"], p["B"], True, p.get("sequence_type", 0))
+    got = {}
+    for b in np.nonzero(kc.bin_sizes())[0].tolist():
+        text = kc.bin_text(b)
+        assert not text.endswith("EOF")
+        got[f"bin{b}"] = sorted(text.splitlines())
+    exp = {b: sorted(t[:-3].splitlines()) for b, t in expected.items()}
+    assert got == exp
+
+
+def test_write_bins_byte_identical(tmp_path):
+    fasta, expected = load_golden("short_reads_k28")
+    kc = run_counter(fasta, 28, 10, 3, 2048)
+    out = tmp_path / "out"
+    kc.write_bins(str(out))
+    files = {f: (out / f).read_text() for f in os.listdir(out)}
+    assert files == expected
+
+
+def test_cli_matches_reference_layout(tmp_path):
+    fasta, expected = load_golden("short_reads_k28")
+    inp = tmp_path / "in.fa"
+    inp.write_bytes(fasta)
+    r = subprocess.run([fk.CLI_PATH, "LocalTestKmerCounter", "28", "10", "3", "2048", "0", "0", str(inp),
+                        str(tmp_path) + "/", "run_", "1", "0", "0"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    outdir = tmp_path / "run_k28_m10_x3_b2048_s0"
+    files = {f: (outdir / f).read_text() for f in os.listdir(outdir)}
+    assert files == expected
+    # useHT=1 writes the same lines without EOF
+    r = subprocess.run([fk.CLI_PATH, "28", "10", "3", "2048", "1", "0", str(inp), str(tmp_path) + "/", "ht_",
+                        "1", "0", "1", "4"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    outdir = tmp_path / "ht_k28_m10_x3_b2048_s0"
+    files = {f: sorted((outdir / f).read_text().splitlines()) for f in os.listdir(outdir)}
+    assert files == {b: sorted(t[:-3].splitlines()) for b, t in expected.items()}
+
+
+def random_fasta(rng, nreads, lo, hi, alphabet="ACGT", noise="", noise_p=0.0, wrap=0):
+    out = []
+    for i in range(nreads):
+        s = "".join(rng.choice(alphabet) for _ in range(rng.randint(lo, hi)))
+        if noise:
+            s = "".join(rng.choice(noise) if rng.random() < noise_p else ch for ch in s)
+        if wrap and s:
+            s = "\n".join(s[q:q + wrap] for q in range(0, len(s), wrap))
+        out.append(f">read{i} some header ACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGT\n{s}\n")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_vs_oracle(seed):
+    rng = random.Random(seed)
+    k = rng.choice([5, 11, 15, 21, 27, 28, 31, 32, 33, 40, 55, 63, 64])
+    m = min(k, rng.choice([1, 2, 3, 5, 7, 9, 10, 12, 15]))
+    B = rng.choice([1, 3, 64, 1000, 2048, 8192])
+    use_ht = bool(seed % 3 == 0)
+    fasta = random_fasta(rng, rng.randint(1, 300), 0, rng.choice([60, 200, 800]),
+                         alphabet=rng.choice(["ACGT", "ACGT", "AC", "GT", "ACGTN"]),
+                         noise=rng.choice(["", "Nn\r", "acgtRY"]), noise_p=0.01, wrap=rng.choice([0, 0, 7, 61]))
+    kc = run_counter(fasta, k, m, 3, B, use_ht)
+    ref = oracle.OracleResult(fasta, k, m, B)
+    assert kc.stats()["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref, ordered=not use_ht)
+
+
+@pytest.mark.parametrize("use_ht", [False, True])
+def test_baseline_c1_synthetic_vs_oracle(use_ht):
+    # BASELINE configs[0]: k=28 m=10 x=3 B=2048, 10 MB synthetic 100 bp reads
+    n_reads = 10_000_000 // 114
+    fasta = fk.synth_fasta(n_reads, 100, 1_000_000, seed=0x5EED)
+    kc = run_counter(fasta, 28, 10, 3, 2048, use_ht)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    assert kc.stats()["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref, ordered=not use_ht)
+
+
+def test_two_word_k55_vs_oracle():
+    # BASELINE configs[3] shape (k=55 m=12, 150 bp) at oracle-friendly size
+    fasta = fk.synth_fasta(20_000, 150, 200_000, seed=11)
+    for use_ht in (False, True):
+        kc = run_counter(fasta, 55, 12, 3, 8192, use_ht)
+        ref = oracle.OracleResult(fasta, 55, 12, 8192)
+        assert_same_as_oracle(kc, ref, ordered=not use_ht)
+
+
+def test_long_sequence_type1_vs_oracle():
+    # BASELINE configs[4] shape: one long record, 60-column lines, N runs, soft-masked lowercase
+    rng = random.Random(5)
+    seq = []
+    for blk in range(40):
+        s = "".join(rng.choice("ACGT") for _ in range(50_000))
+        if blk % 7 == 3:
+            s = s[:1000] + "N" * 3000 + s[4000:]
+        if blk % 5 == 1:
+            s = s[:20_000] + s[20_000:30_000].lower() + s[30_000:]
+        seq.append(s)
+    seq = "".join(seq)
+    fasta = (">chrSynthetic\n" + "\n".join(seq[q:q + 60] for q in range(0, len(seq), 60)) + "\n").encode()
+    kc = run_counter(fasta, 28, 10, 3, 2048, False, sequence_type=1)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048, 1)
+    assert_same_as_oracle(kc, ref)
+
+
+def test_large_bucket_path_vs_oracle(monkeypatch):
+    # every bucket through the streaming global-memory sort (k_bucket_sort_large)
+    monkeypatch.setenv("FASTKMER_DEBUG_LARGE_BUCKETS", "1")
+    fasta = fk.synth_fasta(3000, 100, 20_000, seed=3)
+    for k, m in ((28, 10), (41, 9)):
+        kc = run_counter(fasta, k, m, 3, 16)
+        assert kc.stats()["oversize_buckets"] > 0
+        ref = oracle.OracleResult(fasta, k, m, 16)
+        assert_same_as_oracle(kc, ref)
+
+
+def test_skewed_repeats_vs_oracle():
+    # one k-mer repeated ~100k times, poly-A/poly-C blocks: single cells far above the LDS capacity
+    fasta = (b">a\n" + b"A" * 100_000 + b"\n>b\n" + b"AC" * 60_000 + b"\n>c\n" + b"ACGTTGCA" * 20_000 + b"\n")
+    for use_ht in (False, True):
+        kc = run_counter(fasta, 21, 7, 3, 64, use_ht)
+        ref = oracle.OracleResult(fasta, 21, 7, 64)
+        assert_same_as_oracle(kc, ref, ordered=not use_ht)
+
+
+@pytest.mark.parametrize("data", [b"", b"ACGT\n", b">only\n", b">a\nACG\n>b\n\n>c\nNNNNNNNNNNNNNNNNNNNNNNNNNNNNNNNN\n"])
+def test_empty_and_degenerate(data):
+    kc = run_counter(data, 21, 7, 3, 64)
+    assert int(kc.bin_sizes().sum()) == 0
+    assert kc.stats()["kmers"] == 0
+
+
+def test_multi_rank_in_one_process_matches_single():
+    # the exchange path without RCCL: 3 ranks, records routed by bin % 3
+    fasta = fk.synth_fasta(20_000, 100, 300_000, seed=9)
+    rec = 114
+    G = 3
+    shards = [fasta[r * rec * 7000:(r + 1) * rec * 7000] for r in range(G)]
+    ranks = [fk.KmerCounter(28, 10, 3, 2048, False, 0, n_ranks=G, rank=r) for r in range(G)]
+    import torch
+    sends = []
+    for r in range(G):
+        ranks[r].ingest(shards[r])
+        counts = ranks[r].map()
+        buf = torch.empty(max(sum(counts), 1) * ranks[r].record_bytes, dtype=torch.uint8, device="cuda")
+        ranks[r].map_emit(buf.data_ptr(), max(sum(counts), 1))
+        torch.cuda.synchronize()
+        sends.append((buf, counts))
+    rb = ranks[0].record_bytes
+    for dst in range(G):
+        parts = []
+        for src in range(G):
+            buf, counts = sends[src]
+            off = sum(counts[:dst])
+            parts.append(buf[off * rb:(off + counts[dst]) * rb])
+        recv = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device="cuda")
+        ranks[dst].reduce(recv.data_ptr(), recv.numel() // rb)
+        torch.cuda.synchronize()
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    ref_sizes = ref.bin_sizes()
+    for dst in range(G):
+        sizes = ranks[dst].bin_sizes()
+        for b in range(ref.nbins):
+            if b % G != dst:
+                assert sizes[b] == 0
+                continue
+            assert sizes[b] == ref_sizes[b]
+            if ref_sizes[b]:
+                hi, lo, cnt = counter_arrays(ranks[dst], b)
+                rhi, rlo, rcnt = ref.bin_arrays(b)
+                assert np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
+
+
+def test_device_synth_matches_host():
+    import torch
+    kc = fk.KmerCounter(28, 10, 3, 2048)
+    nb = kc.synth_device(5000, 100, 100_000, seed=42)
+    host = fk.synth_fasta(5000, 100, 100_000, seed=42)
+    assert nb == len(host)
+    kc.finish()
+    ref = oracle.OracleResult(host, 28, 10, 2048)
+    assert_same_as_oracle(kc, ref)
+
+
+def test_full_size_properties():
+    # BASELINE configs[1] (1 GB, k=28 m=10 B=2048) through size-independent properties:
+    # counts sum to the k-mer windows, each bin is strictly ascending, and a sample of
+    # k-mers re-hashes (oracle norm + hash_to_bucket) to the bin it was filed under.
+    n_reads = 1_000_000_000 // 114
+    kc = fk.KmerCounter(28, 10, 3, 2048)
+    kc.synth_device(n_reads, 100, 100_000_000, seed=0x5EED)
+    kc.finish()
+    st = kc.stats()
+    sizes = kc.bin_sizes()
+    total = 0
+    rng = random.Random(0)
+    sample_bins = rng.sample(np.nonzero(sizes)[0].tolist(), 16)
+    for b in sample_bins:
+        keys, counts = kc.get_bin(b)
+        assert np.all(keys[1:] > keys[:-1])
+        for kk in rng.sample(fk.decode_keys(keys, 28), 20):
+            sig = min(oracle.norm(int("".join("%d" % "ACGT".index(ch) for ch in kk[j:j + 10]), 4), 10)
+                      for j in range(19))
+            assert oracle.hash_to_bucket(sig, 2048) == b
+    all_counts = 0
+    for b in np.nonzero(sizes)[0].tolist():
+        _, counts = kc.get_bin(b)
+        all_counts += int(counts.sum(dtype=np.uint64))
+    assert st["distinct"] == int(sizes.sum())
+    assert all_counts == st["kmers"]
+    assert st["kmers"] > 0.9 * n_reads * 73
