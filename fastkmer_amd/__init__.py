@@ -72,6 +72,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m fastkmer_amd.build` "
                            "(there is no CPU fallback)")
+    # One HIP runtime per process: torch ships its own libamdhip64 with the
+    # same SONAME as /opt/rocm's.  Loading torch first makes the dynamic
+    # loader bind libfastkmer.so to that runtime, so device pointers, streams
+    # and RCCL (torch.distributed "nccl") are shared with torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, I32, U64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
     sig = {

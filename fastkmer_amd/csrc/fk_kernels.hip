@@ -314,7 +314,7 @@ __device__ __forceinline__ uint64_t classify64(const uint8_t *fa, uint64_t n, ui
         if (p < n) {
             if (st == ST_LINESTART) {
                 st = (c == '>') ? ST_HDR : ((int64_t)p > fh ? ST_SEQ : ST_JUNK);
-                keep = (st == ST_HDR);  // the '>' of a header separates records
+                keep = (st != ST_JUNK);  // a header keeps its '>' as the record separator
             } else {
                 keep = (st == ST_SEQ) && c != '\n';
             }
