@@ -48,7 +48,7 @@ class fk_config(ctypes.Structure):
 class fk_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("fasta_bytes", "positions", "bases", "kmers", "superkmers", "records_received", "distinct",
-                 "oversize_buckets")] + \
+                 "oversize_buckets", "buckets", "fine_bits")] + \
                [(n, ctypes.c_double) for n in
                 ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
                  "ms_signature_kernel")]

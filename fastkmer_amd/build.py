@@ -20,7 +20,7 @@ ARCH = os.environ.get("FASTKMER_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 LIB_SOURCES = ["fk_kernels.hip", "fk_api.cpp"]
-DEPS = ["fk_kernels.hip", "fk_kernels_part2.inc", "fk_api.cpp", "fk_common.h", "fk_internal.h"]
+DEPS = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".inc", ".h")) or f == "fk_api.cpp")
 
 
 def _stale(target: str, deps: list[str]) -> bool:

@@ -109,6 +109,7 @@ struct fk_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS: route every bucket through 5b
+    int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
 
     // input
     std::vector<uint8_t> host_in;
@@ -117,7 +118,7 @@ struct fk_ctx {
     DevBuf fasta_own;
 
     // parse + encode
-    DevBuf tile_last_nl, tile_prev_nl, tile_kept, tile_off, first_hdr, npos_dev, codes, valid;
+    DevBuf tile_last_nl, tile_prev_nl, tile_first_hdr, tile_kept, tile_off, first_hdr, npos_dev, codes, valid;
     // signature
     DevBuf records, counters;
     uint64_t nrec = 0, nkmers = 0;
@@ -127,7 +128,8 @@ struct fk_ctx {
     std::vector<uint64_t> send_counts;
     // reduce
     DevBuf part_rec, part_kmer, part_off, part_cursor, precs, chunks, bin_chunk_begin;
-    DevBuf chunk_hist, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
+    DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
+    DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc;
     DevBuf table_off, tkeys, tstate, tcounts;
     ScanWorkspace ws;
@@ -252,6 +254,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->fm = make_fastmod((uint32_t)c->Bc);
     const char *dbg = getenv("FASTKMER_DEBUG_LARGE_BUCKETS");
     c->force_large = dbg && dbg[0] == '1';
+    const char *ph = getenv("FASTKMER_DEBUG_PHASE");
+    if (ph && ph[0]) c->dbg_phase = atoi(ph);
     if (cfg->device >= 0) {
         if (cfg->device >= ndev) {
             delete c;
@@ -284,10 +288,11 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_prev_nl, &c->tile_kept, &c->tile_off,
+    DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_prev_nl, &c->tile_first_hdr, &c->tile_kept, &c->tile_off,
                       &c->first_hdr, &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters,
                       &c->dest_rec, &c->dest_kmer, &c->dest_off, &c->dest_cursor, &c->part_rec, &c->part_kmer,
-                      &c->part_off, &c->part_cursor, &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_hist,
+                      &c->part_off, &c->part_cursor, &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk,
+                      &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
@@ -398,6 +403,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     const uint64_t valid_words = n / 32 + 2 * POS_PAD_WORDS + 512;
     FK_TRY(ensure(c->tile_last_nl, ntiles * 8));
     FK_TRY(ensure(c->tile_prev_nl, ntiles * 8));
+    FK_TRY(ensure(c->tile_first_hdr, ntiles * 8));
     FK_TRY(ensure(c->tile_kept, ntiles * 8));
     FK_TRY(ensure(c->tile_off, ntiles * 8));
     FK_TRY(ensure(c->first_hdr, 8));
@@ -413,7 +419,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     HIP_TRY(hipMemsetAsync(c->valid.p, 0, valid_words * 4, s));
     HIP_TRY(hipMemsetAsync(c->npos_dev.p, 0, 8, s));
     if (n) {
-        HIP_TRY(launch_fasta_marks(c->d_fasta, n, c->tile_last_nl.as<int64_t>(),
+        HIP_TRY(launch_fasta_marks(c->d_fasta, n, c->tile_last_nl.as<int64_t>(), c->tile_first_hdr.as<int64_t>(),
                                    c->first_hdr.as<unsigned long long>(), s));
         HIP_TRY(scan_excl_max_i64(c->tile_last_nl.as<int64_t>(), c->tile_prev_nl.as<int64_t>(), ntiles, c->ws, s));
         HIP_TRY(launch_fasta_count(c->d_fasta, n, c->tile_prev_nl.as<int64_t>(),
@@ -513,58 +519,77 @@ FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
 static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint64_t max_bin_kmers) {
     hipStream_t s = c->stream;
     const int k = c->cfg.k;
-    const uint32_t cap = (uint32_t)(SORT_CAP / c->KW);
+    const uint32_t cap = 2048;  // keys per LDS bucket (k_bucket_count64 / 128-bit k_bucket_sort)
     // fine bits: ~8 cells per LDS bucket for the largest bin
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * (cap / 8) < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
+    const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
-    FK_TRY(ensure(c->chunk_hist, (uint64_t)nchunks * (4ull << F)));
+    FK_TRY(ensure(c->chunk_nk, ((uint64_t)nchunks + 1) * 8));
+    FK_TRY(ensure(c->chunk_base, ((uint64_t)nchunks + 1) * 8));
+    FK_TRY(ensure(c->lp, (uint64_t)nchunks * (ncell + 1) * 4));
+    FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->flags, ncell_all * 4));
     FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
-    HIP_TRY(launch_cell_hist(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
-                             c->chunk_hist.as<uint32_t>(), s));
-    HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->chunk_hist.as<uint32_t>(),
+    // 4a/4b: chunk offsets, then expand every record into its chunk's region
+    HIP_TRY(launch_chunk_kmers(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks,
+                               c->chunk_nk.as<uint64_t>(), s));
+    HIP_TRY(scan_excl_sum_u64(c->chunk_nk.as<uint64_t>(), c->chunk_base.as<uint64_t>(), nchunks,
+                              c->chunk_base.as<uint64_t>() + nchunks, c->ws, s));
+    HIP_TRY(launch_expand(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks,
+                          c->chunk_base.as<uint64_t>(), k, F, c->lp.as<uint32_t>(), c->keys.as<uint64_t>(), s));
+    // 4c: cell totals -> output positions -> buckets
+    HIP_TRY(launch_cell_totals(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
                                c->cell_total.as<uint64_t>(), s));
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
                               c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
-    const uint32_t small = cap / 4;
-    const uint32_t group = cap - cap / 4;
-    const uint32_t small_limit = c->force_large ? 0u : cap;
-    HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, small, group,
-                                c->flags.as<uint32_t>(), s));
+    HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
+                                cap - cap / 4, c->flags.as<uint32_t>(), s));
     HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), ncell_all,
                                      c->flag_scan.as<uint64_t>() + ncell_all, c->ws, s));
     uint64_t nbuckets = 0;
     HIP_TRY(hipMemcpyAsync(&nbuckets, c->flag_scan.as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     FK_TRY(ensure(c->buckets, nbuckets * sizeof(Bucket)));
-    FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->out_keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->out_counts, total_kmers * 4));
     FK_TRY(ensure(c->bucket_unique, (nbuckets + 1) * 8));
     FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
     HIP_TRY(launch_bucket_write(c->cell_base.as<uint64_t>(), c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(),
-                                c->nlb, F, total_kmers, c->buckets.as<Bucket>(), s));
-    HIP_TRY(launch_bucket_sizes(c->buckets.as<Bucket>(), nbuckets, total_kmers, s));
-    HIP_TRY(launch_cell_scatter(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
-                                c->chunk_hist.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
-                                s));
+                                c->nlb, F, nbuckets, total_kmers, c->buckets.as<Bucket>(), s));
+    // 5: exact count per bucket in LDS; buckets that do not fit take the streaming path
+    const uint32_t small_limit = c->force_large ? 0u : cap;
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
-    HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
-                               c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                               c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit, s));
+    if (c->KW == 1)
+        HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), c->chunk_base.as<uint64_t>(), c->lp.as<uint32_t>(),
+                                      c->bin_chunk_begin.as<uint32_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+                                      c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                      c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit,
+                                      c->dbg_phase, s));
+    else
+        HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->chunk_base.as<uint64_t>(), c->lp.as<uint32_t>(),
+                                   c->bin_chunk_begin.as<uint32_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+                                   c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                   c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit,
+                                   s));
     uint64_t oversize = 0;
     HIP_TRY(hipMemcpyAsync(&oversize, c->misc.p, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     c->stats.oversize_buckets = oversize;
-    if (oversize)
-        HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+    c->stats.buckets = nbuckets;
+    c->stats.fine_bits = (uint64_t)F;
+    if (oversize) {
+        FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+        HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->chunk_base.as<uint64_t>(),
+                                         c->lp.as<uint32_t>(), c->bin_chunk_begin.as<uint32_t>(), F,
+                                         c->buckets.as<Bucket>(), nbuckets, k, c->scratch.as<uint64_t>(),
                                          c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                         c->bucket_unique.as<uint64_t>(), small_limit, s));
+                                         c->bucket_unique.as<uint64_t>(), s));
+    }
     HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
     uint64_t distinct = 0;

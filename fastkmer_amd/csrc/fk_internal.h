@@ -29,9 +29,10 @@ constexpr int REC_BIN_BITS = 22;
 constexpr uint32_t REC_BIN_MASK = (1u << REC_BIN_BITS) - 1u;
 
 struct Bucket {
-    uint64_t begin;  // first key index (into keys / out_keys)
+    uint64_t begin;  // output position of the bucket's first key (prefix over (bin, cell))
     uint32_t n;      // keys in the bucket
     uint32_t lbin;   // local bin
+    uint32_t c0, c1; // cells [c0, c1) of the bin
 };
 
 struct Chunk {
@@ -53,8 +54,8 @@ hipError_t scan_excl_sum_u32_to_u64(const uint32_t *in, uint64_t *out, uint64_t 
 hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWorkspace &ws, hipStream_t s);
 
 // ---- FASTA parse + encode (records -> compacted packed positions)
-hipError_t launch_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl, unsigned long long *first_hdr,
-                              hipStream_t s);
+hipError_t launch_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl, int64_t *tile_first_hdr,
+                              unsigned long long *first_hdr, hipStream_t s);
 hipError_t launch_fasta_count(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
                               const unsigned long long *first_hdr, uint64_t *tile_kept, hipStream_t s);
 hipError_t launch_fasta_encode(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
@@ -75,29 +76,34 @@ hipError_t launch_part_scatter(int W, const uint64_t *rec, uint64_t nrec, int mo
                                hipStream_t s);
 
 // ---- sorted count
-hipError_t launch_cell_hist(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,
-                            int F, uint32_t *chunk_hist, hipStream_t s);
-hipError_t launch_cell_prefix(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, uint32_t *chunk_hist,
+hipError_t launch_chunk_kmers(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, uint64_t *chunk_nk,
+                              hipStream_t s);
+hipError_t launch_expand(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
+                         const uint64_t *chunk_base, int k, int F, uint32_t *lp, uint64_t *keys, hipStream_t s);
+hipError_t launch_cell_totals(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, const uint32_t *lp,
                               uint64_t *cell_total, hipStream_t s);
 hipError_t launch_bucket_flags(const uint64_t *cell_base, const uint64_t *cell_total, uint32_t nlbins, int F,
                                uint32_t small_cap, uint32_t group, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags, const uint64_t *flag_scan,
-                               uint32_t nlbins, int F, uint64_t total_keys, Bucket *buckets, hipStream_t s);
-hipError_t launch_cell_scatter(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,
-                               int F, const uint32_t *chunk_hist, const uint64_t *cell_base, uint64_t *keys,
+                               uint32_t nlbins, int F, uint64_t nbuckets, uint64_t total_keys, Bucket *buckets,
                                hipStream_t s);
-hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
+hipError_t launch_bucket_count64(const uint64_t *keys, const uint64_t *chunk_base, const uint32_t *lp,
+                                 const uint32_t *bin_chunk_begin, int F, const Bucket *buckets, uint64_t nbuckets,
+                                 int k, uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+                                 unsigned long long *oversize, uint32_t small_limit, int dbg_phase, hipStream_t s);
+hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const uint64_t *chunk_base, const uint32_t *lp,
+                              const uint32_t *bin_chunk_begin, int F, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, hipStream_t s);
-hipError_t launch_bucket_sort_large(int KW, uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
-                                    uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                                    uint32_t small_limit, hipStream_t s);
+hipError_t launch_bucket_sort_large(int KW, const uint64_t *keys, const uint64_t *chunk_base, const uint32_t *lp,
+                                    const uint32_t *bin_chunk_begin, int F, const Bucket *buckets, uint64_t nbuckets,
+                                    int k, uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
+                                    uint64_t *bucket_unique, hipStream_t s);
 hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_t *out_counts,
                                  const Bucket *buckets, uint64_t nbuckets, const uint64_t *dense_off,
                                  uint64_t *dense_keys, uint32_t *dense_counts, hipStream_t s);
 hipError_t launch_bin_offsets(const uint64_t *flag_scan, const uint64_t *dense_off, uint32_t nlbins, int F,
                               uint64_t nbuckets, uint64_t *bin_off, hipStream_t s);
-hipError_t launch_bucket_sizes(Bucket *buckets, uint64_t nb, uint64_t total_keys, hipStream_t s);
 
 // ---- hash count (extractKXmersHT)
 hipError_t launch_ht_insert(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,

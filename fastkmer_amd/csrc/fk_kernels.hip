@@ -255,7 +255,7 @@ __device__ __forceinline__ uint8_t byte_of(const uint32_t (&w)[16], int j) {
 }
 
 __global__ __launch_bounds__(NT) void k_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl,
-                                                    unsigned long long *first_hdr) {
+                                                    int64_t *tile_first_hdr) {
     __shared__ int64_t s_tmp[NT / 64];
     const uint64_t p0 = (uint64_t)blockIdx.x * ENC_TILE + (uint64_t)threadIdx.x * ENC_BPT;
     uint32_t w[16];
@@ -275,8 +275,28 @@ __global__ __launch_bounds__(NT) void k_fasta_marks(const uint8_t *fa, uint64_t 
     }
     int64_t tot;
     (void)block_excl_max<int64_t>(last_nl, (int64_t)-1, s_tmp, &tot);
-    if (threadIdx.x == 0) tile_last_nl[blockIdx.x] = tot;
-    if (hdr != INT64_MAX) atomicMin(first_hdr, (unsigned long long)hdr);
+    // first header of the tile: max over -hdr (one value per tile, no atomics)
+    int64_t neg_first;
+    (void)block_excl_max<int64_t>(-hdr, -INT64_MAX, s_tmp, &neg_first);
+    if (threadIdx.x == 0) {
+        tile_last_nl[blockIdx.x] = tot;
+        tile_first_hdr[blockIdx.x] = -neg_first;
+    }
+}
+
+// first header of the whole input = min over tiles (one workgroup)
+__global__ __launch_bounds__(1024) void k_first_header(const int64_t *tile_first_hdr, uint64_t ntiles,
+                                                       unsigned long long *first_hdr) {
+    __shared__ int64_t s_m[1024];
+    int64_t m = INT64_MAX;
+    for (uint64_t t = threadIdx.x; t < ntiles; t += 1024) m = min(m, tile_first_hdr[t]);
+    s_m[threadIdx.x] = m;
+    __syncthreads();
+    for (int st = 512; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) s_m[threadIdx.x] = min(s_m[threadIdx.x], s_m[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *first_hdr = (unsigned long long)s_m[0];
 }
 
 // State machine shared by the count and encode passes.  Returns the kept
@@ -409,11 +429,12 @@ __global__ __launch_bounds__(NT) void k_fasta_encode(const uint8_t *fa, uint64_t
     }
 }
 
-hipError_t launch_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl, unsigned long long *first_hdr,
-                              hipStream_t s) {
+hipError_t launch_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl, int64_t *tile_first_hdr,
+                              unsigned long long *first_hdr, hipStream_t s) {
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     if (nt == 0) return hipSuccess;
-    k_fasta_marks<<<(unsigned)nt, NT, 0, s>>>(fa, n, tile_last_nl, first_hdr);
+    k_fasta_marks<<<(unsigned)nt, NT, 0, s>>>(fa, n, tile_last_nl, tile_first_hdr);
+    k_first_header<<<1, 1024, 0, s>>>(tile_first_hdr, nt, first_hdr);
     return hipGetLastError();
 }
 
@@ -434,5 +455,13 @@ hipError_t launch_fasta_encode(const uint8_t *fa, uint64_t n, const int64_t *til
     return hipGetLastError();
 }
 
-#include "fk_kernels_part2.inc"
+#include "fk_signature.inc"
+#include "fk_records.inc"
+#include "fk_partition.inc"
+#include "fk_radix_rank.inc"
+#include "fk_count_sorted.inc"
+#include "fk_sort_radix.inc"
+#include "fk_compact.inc"
+#include "fk_count_hash.inc"
+#include "fk_synth.inc"
 }  // namespace fk

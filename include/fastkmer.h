@@ -61,6 +61,8 @@ typedef struct fk_stats {
     uint64_t records_received; /* records counted by fk_reduce */
     uint64_t distinct;         /* distinct canonical k-mers owned by this rank */
     uint64_t oversize_buckets; /* buckets that took the large-bucket path */
+    uint64_t buckets;          /* LDS count buckets (sorted path) */
+    uint64_t fine_bits;        /* cell bits F below the bin (sorted path) */
     double ms_parse;           /* FASTA parse + 2-bit encode kernels */
     double ms_signature;       /* signature / super-k-mer kernel */
     double ms_partition;       /* record partition kernels */

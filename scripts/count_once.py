@@ -1,0 +1,10 @@
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa
+import fastkmer_amd as fk
+kc = fk.KmerCounter(28, 10, 3, 2048)
+kc.synth_device(1_000_000_000 // 114, 100, 100_000_000, seed=0x5EED)
+for i in range(3):
+    kc.finish()
+st = kc.stats()
+print(f"count {st['ms_count']:.2f} ms  buckets {st['buckets']} F {st['fine_bits']} oversize {st['oversize_buckets']} distinct {st['distinct']}")
