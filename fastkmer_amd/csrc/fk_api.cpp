@@ -526,27 +526,22 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     F = std::min(F, 2 * k);
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
-    FK_TRY(ensure(c->chunk_nk, ((uint64_t)nchunks + 1) * 8));
-    FK_TRY(ensure(c->chunk_base, ((uint64_t)nchunks + 1) * 8));
-    FK_TRY(ensure(c->lp, (uint64_t)nchunks * (ncell + 1) * 4));
+    FK_TRY(ensure(c->lp, (uint64_t)nchunks * ncell * 4));
     FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->flags, ncell_all * 4));
     FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
-    // 4a/4b: chunk offsets, then expand every record into its chunk's region
-    HIP_TRY(launch_chunk_kmers(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks,
-                               c->chunk_nk.as<uint64_t>(), s));
-    HIP_TRY(scan_excl_sum_u64(c->chunk_nk.as<uint64_t>(), c->chunk_base.as<uint64_t>(), nchunks,
-                              c->chunk_base.as<uint64_t>() + nchunks, c->ws, s));
-    HIP_TRY(launch_expand(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks,
-                          c->chunk_base.as<uint64_t>(), k, F, c->lp.as<uint32_t>(), c->keys.as<uint64_t>(), s));
-    // 4c: cell totals -> output positions -> buckets
-    HIP_TRY(launch_cell_totals(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
+    // 4: expand records -> canonical k-mers, laid out bin-major by cell
+    HIP_TRY(launch_expand_hist(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+                               c->lp.as<uint32_t>(), s));
+    HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
                                c->cell_total.as<uint64_t>(), s));
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
                               c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
+    HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+                                  c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(), s));
     HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
                                 cap - cap / 4, c->flags.as<uint32_t>(), s));
     HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), ncell_all,
@@ -565,14 +560,12 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     const uint32_t small_limit = c->force_large ? 0u : cap;
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
     if (c->KW == 1)
-        HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), c->chunk_base.as<uint64_t>(), c->lp.as<uint32_t>(),
-                                      c->bin_chunk_begin.as<uint32_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+        HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
                                       c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                       c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit,
                                       c->dbg_phase, s));
     else
-        HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->chunk_base.as<uint64_t>(), c->lp.as<uint32_t>(),
-                                   c->bin_chunk_begin.as<uint32_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+        HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
                                    c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                    c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit,
                                    s));
@@ -584,9 +577,8 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     c->stats.fine_bits = (uint64_t)F;
     if (oversize) {
         FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-        HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->chunk_base.as<uint64_t>(),
-                                         c->lp.as<uint32_t>(), c->bin_chunk_begin.as<uint32_t>(), F,
-                                         c->buckets.as<Bucket>(), nbuckets, k, c->scratch.as<uint64_t>(),
+        HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+                                         c->scratch.as<uint64_t>(),
                                          c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                          c->bucket_unique.as<uint64_t>(), s));
     }

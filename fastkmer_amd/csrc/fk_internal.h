@@ -76,28 +76,25 @@ hipError_t launch_part_scatter(int W, const uint64_t *rec, uint64_t nrec, int mo
                                hipStream_t s);
 
 // ---- sorted count
-hipError_t launch_chunk_kmers(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, uint64_t *chunk_nk,
-                              hipStream_t s);
-hipError_t launch_expand(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
-                         const uint64_t *chunk_base, int k, int F, uint32_t *lp, uint64_t *keys, hipStream_t s);
-hipError_t launch_cell_totals(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, const uint32_t *lp,
+hipError_t launch_expand_hist(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
+                              uint32_t *hist, hipStream_t s);
+hipError_t launch_cell_prefix(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, uint32_t *hist,
                               uint64_t *cell_total, hipStream_t s);
+hipError_t launch_expand_scatter(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
+                                 const uint32_t *hist, const uint64_t *cell_base, uint64_t *keys, hipStream_t s);
 hipError_t launch_bucket_flags(const uint64_t *cell_base, const uint64_t *cell_total, uint32_t nlbins, int F,
                                uint32_t small_cap, uint32_t group, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags, const uint64_t *flag_scan,
                                uint32_t nlbins, int F, uint64_t nbuckets, uint64_t total_keys, Bucket *buckets,
                                hipStream_t s);
-hipError_t launch_bucket_count64(const uint64_t *keys, const uint64_t *chunk_base, const uint32_t *lp,
-                                 const uint32_t *bin_chunk_begin, int F, const Bucket *buckets, uint64_t nbuckets,
-                                 int k, uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
+                                 uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase, hipStream_t s);
-hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const uint64_t *chunk_base, const uint32_t *lp,
-                              const uint32_t *bin_chunk_begin, int F, const Bucket *buckets, uint64_t nbuckets, int k,
+hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, hipStream_t s);
-hipError_t launch_bucket_sort_large(int KW, const uint64_t *keys, const uint64_t *chunk_base, const uint32_t *lp,
-                                    const uint32_t *bin_chunk_begin, int F, const Bucket *buckets, uint64_t nbuckets,
-                                    int k, uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
+hipError_t launch_bucket_sort_large(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
+                                    uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
                                     uint64_t *bucket_unique, hipStream_t s);
 hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_t *out_counts,
                                  const Bucket *buckets, uint64_t nbuckets, const uint64_t *dense_off,
