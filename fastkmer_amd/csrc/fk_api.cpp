@@ -94,7 +94,7 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-constexpr uint32_t CHUNK_RECORDS = 4096;  // records per expansion workgroup (never spans two bins)
+constexpr uint32_t CHUNK_RECORDS = 16384;  // records per expansion workgroup (never spans two bins)
 
 }  // namespace
 
@@ -520,9 +520,11 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     hipStream_t s = c->stream;
     const int k = c->cfg.k;
     const uint32_t cap = 2048;  // keys per LDS bucket (k_bucket_count64 / 128-bit k_bucket_sort)
-    // fine bits: ~8 cells per LDS bucket for the largest bin
+    // cell bits: the largest bin's cells average cap/4 keys (a bucket groups a
+    // few cells; runs of one chunk's keys per cell stay long enough to be
+    // written as whole lines)
     int F = 1;
-    while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * (cap / 8) < max_bin_kmers) ++F;
+    while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * (cap / 4) < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;

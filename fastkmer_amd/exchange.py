@@ -1,12 +1,13 @@
 """Signature->bin shuffle across ranks (replaces Spark's reduceByKey, SBKC:1035).
 
 One process per GPU.  Each rank packs its super-k-mer records grouped by
-destination rank (bin % world, round-robin bin ownership) with
+destination rank (bin % world: bins are owned round-robin) with
 ``fk_map_emit``; one ``all_to_all_single`` of per-destination record counts
-and one ``all_to_all_single`` of the packed records (RCCL over xGMI with the
-"nccl" backend, gloo on CPU tensors in tests) deliver every record to the rank
-that owns its bin, which then runs ``fk_reduce``.  There is no other
-collective on the data path.
+and one ``all_to_all_single`` of the packed records deliver every record to
+the rank that owns its bin, which then runs ``fk_reduce``.  With the "nccl"
+backend (RCCL over xGMI on MI355X) the records move GPU to GPU; with "gloo"
+(CPU-only tests, or ranks sharing one GPU) they are staged through host
+memory.  There is no other collective on the data path.
 """
 from __future__ import annotations
 
@@ -14,24 +15,37 @@ import torch
 import torch.distributed as dist
 
 
+def owner_of_bin(b: int, world: int) -> int:
+    """Rank that counts bin b (round-robin ownership)."""
+    return b % world
+
+
 def exchange_records(send: torch.Tensor, send_counts: list[int], record_bytes: int, group=None):
     """All-to-all of packed records.
 
-    send: uint8 tensor holding sum(send_counts) records, grouped by destination
-    rank (rank 0 first).  Returns (recv uint8 tensor, recv_counts list).
+    ``send`` is a uint8 tensor holding sum(send_counts) records grouped by
+    destination rank (rank 0 first).  Returns (recv, recv_counts) on the same
+    device as ``send``.  Works with "nccl" (device tensors) and "gloo" (host
+    tensors; device tensors are staged through host memory).
     """
     world = dist.get_world_size(group)
-    assert len(send_counts) == world
+    if len(send_counts) != world:
+        raise ValueError(f"send_counts has {len(send_counts)} entries for {world} ranks")
+    if send.numel() != sum(send_counts) * record_bytes:
+        raise ValueError("send buffer size does not match send_counts")
     dev = send.device
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+    host = dist.get_backend(group) == "gloo"
+    wire = torch.device("cpu") if host else dev
+    payload = send.to(wire) if host else send
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(v) for v in rc.cpu().tolist()]
-    recv = torch.empty(sum(recv_counts) * record_bytes, dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(recv, send,
+    recv_counts = [int(v) for v in rc.tolist()]
+    recv = torch.empty(sum(recv_counts) * record_bytes, dtype=torch.uint8, device=wire)
+    dist.all_to_all_single(recv, payload,
                            output_split_sizes=[c * record_bytes for c in recv_counts],
                            input_split_sizes=[c * record_bytes for c in send_counts], group=group)
-    return recv, recv_counts
+    return (recv.to(dev) if host else recv), recv_counts
 
 
 def count_distributed(counter, group=None, device=None):
