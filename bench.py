@@ -76,22 +76,27 @@ def main() -> None:
     ap.add_argument("--bytes-per-gpu", type=int, default=FASTA_BYTES_PER_GPU)
     ap.add_argument("--cpu-sample-bytes", type=int, default=64_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo stages records through host memory "
+                         "(rehearsal of N > 1 with ranks sharing a GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    gpu = local_rank if args.backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if distributed:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local_rank)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     n_reads = args.bytes_per_gpu // REC_BYTES
     kc = fk.KmerCounter(K, M, X, B, use_ht=False, sequence_type=0, n_ranks=world, rank=rank,
-                        device=local_rank)
+                        device=gpu)
     # per-rank shard of one synthetic read set (weak scaling: 1 GB per GPU)
     fasta_bytes = kc.synth_device(n_reads, READ_LEN, GENOME, seed=SEED, first_read=rank * n_reads)
     bases_per_rank = n_reads * READ_LEN
@@ -120,7 +125,7 @@ def main() -> None:
         stats = st
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())

@@ -65,3 +65,31 @@ def count_distributed(counter, group=None, device=None):
     torch.cuda.synchronize(dev)
     counter.reduce(recv.data_ptr(), sum(recv_counts))
     return sum(recv_counts)
+
+
+def execute_job_distributed(configuration, group=None, device=None):
+    """SparkBinKmerCounter.executeJob (SBKC:989-1046) for one rank of a job.
+
+    Every rank reads the dataset, keeps its shard (fastkmer_amd.sharding),
+    maps, exchanges records with the other ranks and counts the bins it owns
+    (bin % world == rank); with ``configuration.write`` each rank writes its
+    own ``bin<b>`` files into the shared output directory, as the Spark
+    executors do.  Returns the rank's KmerCounter.
+    """
+    import fastkmer_amd as fk
+    from fastkmer_amd.sharding import shard_fasta
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    with open(configuration.dataset, "rb") as f:
+        data = f.read()
+    piece = shard_fasta(data, world, rank, configuration.sequenceType, configuration.k)
+    del data
+    kc = fk.KmerCounter(configuration.k, configuration.m, configuration.x, configuration.max_b,
+                        configuration.useHT, configuration.sequenceType, n_ranks=world, rank=rank,
+                        device=dev.index if dev.index is not None else -1)
+    kc.ingest(piece)
+    count_distributed(kc, group=group, device=dev)
+    if configuration.write:
+        kc.write_bins(configuration.outputDir)
+    return kc
