@@ -25,7 +25,7 @@ import re
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libfastkmer.so")
+LIB_PATH = os.environ.get("FASTKMER_LIB") or os.path.join(_PKG, "lib", "libfastkmer.so")
 CLI_PATH = os.path.join(_PKG, "bin", "fastkmer-cli")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "fastkmer.h")
 

@@ -120,7 +120,7 @@ struct fk_ctx {
     // parse + encode
     DevBuf tile_last_nl, tile_prev_nl, tile_first_hdr, tile_kept, tile_off, first_hdr, npos_dev, codes, valid;
     // signature
-    DevBuf records, counters;
+    DevBuf records, counters, sig_status, sig_kmers;
     uint64_t nrec = 0, nkmers = 0;
     bool mapped = false;
     // destination partition (n_ranks > 1)
@@ -289,7 +289,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_prev_nl, &c->tile_first_hdr, &c->tile_kept, &c->tile_off,
-                      &c->first_hdr, &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters,
+                      &c->first_hdr, &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
                       &c->dest_rec, &c->dest_kmer, &c->dest_off, &c->dest_cursor, &c->part_rec, &c->part_kmer,
                       &c->part_off, &c->part_cursor, &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk,
                       &c->chunk_base, &c->lp, &c->scratch,
@@ -411,6 +411,9 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     FK_TRY(ensure(c->codes, code_words * 4));
     FK_TRY(ensure(c->valid, valid_words * 4));
     FK_TRY(ensure(c->counters, 64));
+    const uint64_t sig_tiles = (n + SIG_TILE - 1) / SIG_TILE + 1;
+    FK_TRY(ensure(c->sig_status, sig_tiles * 8));
+    FK_TRY(ensure(c->sig_kmers, sig_tiles * 8));
 
     // 1. FASTA parse + 2-bit encode
     HIP_TRY(hipEventRecord(c->ev[0], s));
@@ -441,11 +444,17 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         rec_cap = c->records.bytes / (c->W * 8);
         HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
         HIP_TRY(hipEventRecord(c->ev[2], s));
+        HIP_TRY(hipMemsetAsync(c->sig_status.p, 0, sig_tiles * 8, s));
+        HIP_TRY(hipMemsetAsync(c->sig_kmers.p, 0, sig_tiles * 8, s));
         HIP_TRY(hipEventRecord(c->ev[10], s));
         HIP_TRY(launch_superkmers(c->W, c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), n,
                                   c->npos_dev.as<uint64_t>(), c->cfg.k, c->cfg.m, c->fm, c->records.as<uint64_t>(),
-                                  rec_cap, c->counters.as<unsigned long long>(), s));
+                                  rec_cap, c->sig_status.as<uint64_t>(), c->sig_kmers.as<uint64_t>(),
+                                  c->counters.as<unsigned long long>(), s));
         HIP_TRY(hipEventRecord(c->ev[11], s));
+        // total k-mers = sum of the per-tile counts (into counters[1])
+        HIP_TRY(scan_excl_sum_u64(c->sig_kmers.as<uint64_t>(), c->sig_status.as<uint64_t>(), sig_tiles,
+                                  c->counters.as<uint64_t>() + 1, c->ws, s));
         HIP_TRY(hipEventRecord(c->ev[3], s));
         uint64_t h[2];
         HIP_TRY(hipMemcpyAsync(h, c->counters.p, 16, hipMemcpyDeviceToHost, s));

@@ -65,7 +65,7 @@ hipError_t launch_fasta_encode(const uint8_t *fa, uint64_t n, const int64_t *til
 // ---- signature + super-k-mer records
 hipError_t launch_superkmers(int W, const uint32_t *codes, const uint32_t *valid, uint64_t npos_bound,
                              const uint64_t *npos_dev, int k, int m, FastMod fm, uint64_t *records, uint64_t rec_cap,
-                             unsigned long long *counters, hipStream_t s);
+                             uint64_t *status, uint64_t *tile_kmers, unsigned long long *counters, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, uint64_t n, uint64_t v, hipStream_t s);
 
 // ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]

@@ -62,6 +62,52 @@ __device__ __forceinline__ T block_excl_sum(T v, T *s_tmp /*[4]*/, T *total) {
     return off + inc - v;
 }
 
+// ---- decoupled look-back (single-pass tile prefix without a shared counter)
+// status[t] = flag << 62 | value: flag 1 = tile aggregate, 2 = inclusive
+// prefix.  Agent-scope atomic loads/stores keep the 8 XCD L2s coherent.
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1ull;
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by one whole wave.  Publishes `agg` for `tile`, returns the sum of
+// the aggregates of tiles 0..tile-1 and publishes the inclusive prefix.
+// Tiles are dispatched in blockIdx order, so every predecessor is resident
+// or finished and the spin terminates.
+__device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg) {
+    const int lane = threadIdx.x & 63;
+    if (tile == 0) {
+        if (lane == 0) lb_store(&status[0], LB_INC | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(&status[tile], LB_AGG | agg);
+    uint64_t excl = 0;
+    int64_t pos = (int64_t)tile - 1;
+    while (true) {
+        const int64_t q = pos - lane;
+        const uint64_t st = q >= 0 ? lb_load(&status[q]) : LB_INC;  // before tile 0: inclusive 0
+        const uint32_t flag = (uint32_t)(st >> 62);
+        const uint64_t inc_mask = __ballot(flag == 2u);
+        const uint64_t zero_mask = __ballot(flag == 0u);
+        const int first_inc = inc_mask ? __builtin_ctzll(inc_mask) : 64;
+        const uint64_t before = first_inc == 64 ? ~0ull : ((1ull << first_inc) - 1ull);
+        if (zero_mask & before) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const uint64_t v = lane <= first_inc ? (st & LB_VAL) : 0ull;
+        excl += __shfl(wave_incl_sum(v), 63, 64);
+        if (first_inc < 64) break;
+        pos -= 64;
+    }
+    if (lane == 0) lb_store(&status[tile], LB_INC | (excl + agg));
+    return excl;
+}
+
 // exclusive block prefix max (identity `ident`)
 template <typename T>
 __device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[4]*/, T *total) {
