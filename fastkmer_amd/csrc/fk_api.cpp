@@ -118,7 +118,7 @@ struct fk_ctx {
     DevBuf fasta_own;
 
     // parse + encode
-    DevBuf tile_last_nl, tile_prev_nl, tile_first_hdr, tile_kept, tile_off, first_hdr, npos_dev, codes, valid;
+    DevBuf tile_last_nl, tile_off, npos_dev, codes, valid;
     // signature
     DevBuf records, counters, sig_status, sig_kmers;
     uint64_t nrec = 0, nkmers = 0;
@@ -288,8 +288,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_prev_nl, &c->tile_first_hdr, &c->tile_kept, &c->tile_off,
-                      &c->first_hdr, &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
+    DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
+                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
                       &c->dest_rec, &c->dest_kmer, &c->dest_off, &c->dest_cursor, &c->part_rec, &c->part_kmer,
                       &c->part_off, &c->part_cursor, &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk,
                       &c->chunk_base, &c->lp, &c->scratch,
@@ -401,12 +401,8 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     const uint64_t ntiles = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t code_words = n / 16 + 2 * POS_PAD_WORDS + 512;
     const uint64_t valid_words = n / 32 + 2 * POS_PAD_WORDS + 512;
-    FK_TRY(ensure(c->tile_last_nl, ntiles * 8));
-    FK_TRY(ensure(c->tile_prev_nl, ntiles * 8));
-    FK_TRY(ensure(c->tile_first_hdr, ntiles * 8));
-    FK_TRY(ensure(c->tile_kept, ntiles * 8));
-    FK_TRY(ensure(c->tile_off, ntiles * 8));
-    FK_TRY(ensure(c->first_hdr, 8));
+    FK_TRY(ensure(c->tile_last_nl, ntiles * 8));  // look-back status: newline / header state
+    FK_TRY(ensure(c->tile_off, ntiles * 8));      // look-back status: output positions
     FK_TRY(ensure(c->npos_dev, 8));
     FK_TRY(ensure(c->codes, code_words * 4));
     FK_TRY(ensure(c->valid, valid_words * 4));
@@ -417,22 +413,15 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
 
     // 1. FASTA parse + 2-bit encode
     HIP_TRY(hipEventRecord(c->ev[0], s));
-    HIP_TRY(launch_fill_u64(c->first_hdr.as<uint64_t>(), 1, (uint64_t)INT64_MAX, s));
     HIP_TRY(hipMemsetAsync(c->codes.p, 0, code_words * 4, s));
     HIP_TRY(hipMemsetAsync(c->valid.p, 0, valid_words * 4, s));
     HIP_TRY(hipMemsetAsync(c->npos_dev.p, 0, 8, s));
     if (n) {
-        HIP_TRY(launch_fasta_marks(c->d_fasta, n, c->tile_last_nl.as<int64_t>(), c->tile_first_hdr.as<int64_t>(),
-                                   c->first_hdr.as<unsigned long long>(), s));
-        HIP_TRY(scan_excl_max_i64(c->tile_last_nl.as<int64_t>(), c->tile_prev_nl.as<int64_t>(), ntiles, c->ws, s));
-        HIP_TRY(launch_fasta_count(c->d_fasta, n, c->tile_prev_nl.as<int64_t>(),
-                                   c->first_hdr.as<unsigned long long>(), c->tile_kept.as<uint64_t>(), s));
-        HIP_TRY(scan_excl_sum_u64(c->tile_kept.as<uint64_t>(), c->tile_off.as<uint64_t>(), ntiles,
-                                  c->npos_dev.as<uint64_t>(), c->ws, s));
+        HIP_TRY(hipMemsetAsync(c->tile_last_nl.p, 0, ntiles * 8, s));
+        HIP_TRY(hipMemsetAsync(c->tile_off.p, 0, ntiles * 8, s));
         HIP_TRY(hipEventRecord(c->ev[8], s));
-        HIP_TRY(launch_fasta_encode(c->d_fasta, n, c->tile_prev_nl.as<int64_t>(),
-                                    c->first_hdr.as<unsigned long long>(), c->tile_off.as<uint64_t>(),
-                                    c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), s));
+        HIP_TRY(launch_fasta_parse(c->d_fasta, n, c->tile_last_nl.as<uint64_t>(), c->tile_off.as<uint64_t>(),
+                                   c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), c->npos_dev.as<uint64_t>(), s));
         HIP_TRY(hipEventRecord(c->ev[9], s));
     }
     HIP_TRY(hipEventRecord(c->ev[1], s));

@@ -74,22 +74,29 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Called by one whole wave.  Publishes `agg` for `tile`, returns the sum of
-// the aggregates of tiles 0..tile-1 and publishes the inclusive prefix.
+struct LbSum {
+    static constexpr uint64_t ident = 0;
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+};
+
+// Called by one whole wave.  Publishes `agg` for `tile`, returns the
+// combination (commutative, associative `op`) of the aggregates of tiles
+// 0..tile-1 and publishes the inclusive value.  Values stay below 2^62.
 // Tiles are dispatched in blockIdx order, so every predecessor is resident
 // or finished and the spin terminates.
-__device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg) {
+template <class Op>
+__device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg, Op op) {
     const int lane = threadIdx.x & 63;
     if (tile == 0) {
         if (lane == 0) lb_store(&status[0], LB_INC | agg);
-        return 0;
+        return Op::ident;
     }
     if (lane == 0) lb_store(&status[tile], LB_AGG | agg);
-    uint64_t excl = 0;
+    uint64_t excl = Op::ident;
     int64_t pos = (int64_t)tile - 1;
     while (true) {
         const int64_t q = pos - lane;
-        const uint64_t st = q >= 0 ? lb_load(&status[q]) : LB_INC;  // before tile 0: inclusive 0
+        const uint64_t st = q >= 0 ? lb_load(&status[q]) : (LB_INC | Op::ident);  // before tile 0
         const uint32_t flag = (uint32_t)(st >> 62);
         const uint64_t inc_mask = __ballot(flag == 2u);
         const uint64_t zero_mask = __ballot(flag == 0u);
@@ -99,12 +106,14 @@ __device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg)
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        const uint64_t v = lane <= first_inc ? (st & LB_VAL) : 0ull;
-        excl += __shfl(wave_incl_sum(v), 63, 64);
+        uint64_t v = lane <= first_inc ? (st & LB_VAL) : Op::ident;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) v = op(v, (uint64_t)__shfl_xor(v, d, 64));
+        excl = op(excl, v);
         if (first_inc < 64) break;
         pos -= 64;
     }
-    if (lane == 0) lb_store(&status[tile], LB_INC | (excl + agg));
+    if (lane == 0) lb_store(&status[tile], LB_INC | op(excl, agg));
     return excl;
 }
 
@@ -258,249 +267,7 @@ hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWo
                                                     ws.bytes, s);
 }
 
-// ---------------------------------------------------------------------------
-// 1. FASTA parse + encode
-//
-// A workgroup owns ENC_TILE bytes; each thread 64 consecutive bytes.  A line
-// is a header iff its first byte is '>'; lines before the first header are
-// ignored; sequence lines are concatenated with '\n' removed; each header
-// contributes one invalid position (its '>') so k-mers never span records.
-// ---------------------------------------------------------------------------
-
-constexpr int ENC_BPT = ENC_TILE / NT;  // 64 bytes per thread
-enum : int { ST_JUNK = 0, ST_HDR = 1, ST_SEQ = 2, ST_LINESTART = 3 };
-
-// 64 bytes of the tile into registers (16 B vector loads when in bounds)
-__device__ __forceinline__ void load64(const uint8_t *fa, uint64_t n, uint64_t p0, uint32_t (&w)[16]) {
-    if (p0 + 64 <= n && ((reinterpret_cast<uintptr_t>(fa + p0) & 15) == 0)) {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(fa + p0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4 q = __builtin_nontemporal_load(src + i);
-            w[4 * i + 0] = q.x;
-            w[4 * i + 1] = q.y;
-            w[4 * i + 2] = q.z;
-            w[4 * i + 3] = q.w;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            uint32_t x = 0;
-            for (int b = 0; b < 4; ++b) {
-                uint64_t p = p0 + 4 * i + b;
-                if (p < n) x |= (uint32_t)fa[p] << (8 * b);
-            }
-            w[i] = x;
-        }
-    }
-}
-
-__device__ __forceinline__ uint8_t byte_of(const uint32_t (&w)[16], int j) {
-    return (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-}
-
-__global__ __launch_bounds__(NT) void k_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl,
-                                                    int64_t *tile_first_hdr) {
-    __shared__ int64_t s_tmp[NT / 64];
-    const uint64_t p0 = (uint64_t)blockIdx.x * ENC_TILE + (uint64_t)threadIdx.x * ENC_BPT;
-    uint32_t w[16];
-    load64(fa, n, p0, w);
-    uint8_t prev = (p0 == 0) ? (uint8_t)'\n' : (p0 - 1 < n ? fa[p0 - 1] : 0);
-    int64_t last_nl = -1;
-    int64_t hdr = INT64_MAX;
-#pragma unroll
-    for (int j = 0; j < ENC_BPT; ++j) {
-        const uint8_t c = byte_of(w, j);
-        const uint64_t p = p0 + j;
-        if (p < n) {
-            if (c == '\n') last_nl = (int64_t)p;
-            if (c == '>' && prev == '\n' && hdr == INT64_MAX) hdr = (int64_t)p;
-        }
-        prev = c;
-    }
-    int64_t tot;
-    (void)block_excl_max<int64_t>(last_nl, (int64_t)-1, s_tmp, &tot);
-    // first header of the tile: max over -hdr (one value per tile, no atomics)
-    int64_t neg_first;
-    (void)block_excl_max<int64_t>(-hdr, -INT64_MAX, s_tmp, &neg_first);
-    if (threadIdx.x == 0) {
-        tile_last_nl[blockIdx.x] = tot;
-        tile_first_hdr[blockIdx.x] = -neg_first;
-    }
-}
-
-// first header of the whole input = min over tiles (one workgroup)
-__global__ __launch_bounds__(1024) void k_first_header(const int64_t *tile_first_hdr, uint64_t ntiles,
-                                                       unsigned long long *first_hdr) {
-    __shared__ int64_t s_m[1024];
-    int64_t m = INT64_MAX;
-    for (uint64_t t = threadIdx.x; t < ntiles; t += 1024) m = min(m, tile_first_hdr[t]);
-    s_m[threadIdx.x] = m;
-    __syncthreads();
-    for (int st = 512; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) s_m[threadIdx.x] = min(s_m[threadIdx.x], s_m[threadIdx.x + st]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *first_hdr = (unsigned long long)s_m[0];
-}
-
-// State machine shared by the count and encode passes.  Returns the kept
-// mask: bit j set = byte j of this thread is a sequence position.
-
-__device__ __forceinline__ int line_state_at(const uint8_t *fa, uint64_t n, int64_t ls, int64_t fh) {
-    // state of the line that starts at ls (ls < n)
-    if (fa[ls] == '>') return ST_HDR;
-    return ls > fh ? ST_SEQ : ST_JUNK;
-}
-
-__device__ __forceinline__ uint64_t classify64(const uint8_t *fa, uint64_t n, uint64_t p0, const uint32_t (&w)[16],
-                                               int64_t tile_prev_nl, int64_t fh, int64_t *s_tmp) {
-    // last '\n' before this thread's first byte: max over earlier threads of the tile, else the tile's carry
-    int64_t my_last = -1;
-#pragma unroll
-    for (int j = 0; j < ENC_BPT; ++j)
-        if (p0 + j < n && byte_of(w, j) == '\n') my_last = (int64_t)(p0 + j);
-    int64_t tot;
-    int64_t prev_nl = block_excl_max<int64_t>(my_last, (int64_t)-1, s_tmp, &tot);
-    if (prev_nl < tile_prev_nl) prev_nl = tile_prev_nl;
-    const int64_t ls = prev_nl + 1;  // start of the line holding byte p0
-    int st;
-    if ((uint64_t)ls == p0) {
-        st = ST_LINESTART;
-    } else {
-        st = ((uint64_t)ls < n) ? line_state_at(fa, n, ls, fh) : ST_JUNK;
-    }
-    uint64_t kept = 0;
-#pragma unroll
-    for (int j = 0; j < ENC_BPT; ++j) {
-        const uint64_t p = p0 + j;
-        const uint8_t c = byte_of(w, j);
-        bool keep = false;
-        if (p < n) {
-            if (st == ST_LINESTART) {
-                st = (c == '>') ? ST_HDR : ((int64_t)p > fh ? ST_SEQ : ST_JUNK);
-                keep = (st != ST_JUNK);  // a header keeps its '>' as the record separator
-            } else {
-                keep = (st == ST_SEQ) && c != '\n';
-            }
-            if (c == '\n') {
-                st = ST_LINESTART;
-                keep = false;
-            }
-        }
-        if (keep) kept |= 1ull << j;
-    }
-    return kept;
-}
-
-__global__ __launch_bounds__(NT) void k_fasta_count(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
-                                                    const unsigned long long *first_hdr, uint64_t *tile_kept) {
-    __shared__ int64_t s_tmp[NT / 64];
-    __shared__ uint64_t s_sum[NT / 64];
-    const uint64_t p0 = (uint64_t)blockIdx.x * ENC_TILE + (uint64_t)threadIdx.x * ENC_BPT;
-    uint32_t w[16];
-    load64(fa, n, p0, w);
-    const int64_t fh = (int64_t)*first_hdr;
-    const uint64_t kept = classify64(fa, n, p0, w, tile_prev_nl[blockIdx.x], fh, s_tmp);
-    uint64_t tot;
-    (void)block_excl_sum<uint64_t>((uint64_t)__popcll(kept), s_sum, &tot);
-    if (threadIdx.x == 0) tile_kept[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(NT) void k_fasta_encode(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
-                                                     const unsigned long long *first_hdr, const uint64_t *tile_off,
-                                                     uint32_t *codes, uint32_t *valid) {
-    __shared__ int64_t s_tmp[NT / 64];
-    __shared__ uint64_t s_sum[NT / 64];
-    __shared__ uint8_t s_out[ENC_TILE + 64];
-    const uint64_t p0 = (uint64_t)blockIdx.x * ENC_TILE + (uint64_t)threadIdx.x * ENC_BPT;
-    uint32_t w[16];
-    load64(fa, n, p0, w);
-    const int64_t fh = (int64_t)*first_hdr;
-    const uint64_t kept = classify64(fa, n, p0, w, tile_prev_nl[blockIdx.x], fh, s_tmp);
-    uint64_t tot;
-    const uint64_t my_off = block_excl_sum<uint64_t>((uint64_t)__popcll(kept), s_sum, &tot);
-    // compact this thread's kept codes into LDS
-    uint32_t q = (uint32_t)my_off;
-#pragma unroll
-    for (int j = 0; j < ENC_BPT; ++j)
-        if ((kept >> j) & 1) s_out[q++] = (uint8_t)base_code(byte_of(w, j));
-    __syncthreads();
-    const uint64_t P0 = tile_off[blockIdx.x];
-    const uint64_t K = tot;
-    if (K == 0) return;
-    // code words: 16 positions per word, MSB-first
-    {
-        const uint64_t wb = P0 >> 4, we = (P0 + K - 1) >> 4;
-        for (uint64_t wi = wb + threadIdx.x; wi <= we; wi += NT) {
-            uint32_t word = 0;
-            bool partial = false;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint64_t gp = (wi << 4) + j;
-                if (gp >= P0 && gp < P0 + K) {
-                    const uint32_t c = s_out[gp - P0];
-                    word |= (c & 3u) << (30 - 2 * j);
-                } else {
-                    partial = true;
-                }
-            }
-            if (partial)
-                atomicOr(&codes[wi], word);
-            else
-                codes[wi] = word;
-        }
-    }
-    // valid words: 32 positions per word, MSB-first
-    {
-        const uint64_t wb = P0 >> 5, we = (P0 + K - 1) >> 5;
-        for (uint64_t wi = wb + threadIdx.x; wi <= we; wi += NT) {
-            uint32_t word = 0;
-            bool partial = false;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const uint64_t gp = (wi << 5) + j;
-                if (gp >= P0 && gp < P0 + K) {
-                    if (s_out[gp - P0] < 4) word |= 1u << (31 - j);
-                } else {
-                    partial = true;
-                }
-            }
-            if (partial)
-                atomicOr(&valid[wi], word);
-            else
-                valid[wi] = word;
-        }
-    }
-}
-
-hipError_t launch_fasta_marks(const uint8_t *fa, uint64_t n, int64_t *tile_last_nl, int64_t *tile_first_hdr,
-                              unsigned long long *first_hdr, hipStream_t s) {
-    const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
-    if (nt == 0) return hipSuccess;
-    k_fasta_marks<<<(unsigned)nt, NT, 0, s>>>(fa, n, tile_last_nl, tile_first_hdr);
-    k_first_header<<<1, 1024, 0, s>>>(tile_first_hdr, nt, first_hdr);
-    return hipGetLastError();
-}
-
-hipError_t launch_fasta_count(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
-                              const unsigned long long *first_hdr, uint64_t *tile_kept, hipStream_t s) {
-    const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
-    if (nt == 0) return hipSuccess;
-    k_fasta_count<<<(unsigned)nt, NT, 0, s>>>(fa, n, tile_prev_nl, first_hdr, tile_kept);
-    return hipGetLastError();
-}
-
-hipError_t launch_fasta_encode(const uint8_t *fa, uint64_t n, const int64_t *tile_prev_nl,
-                               const unsigned long long *first_hdr, const uint64_t *tile_off, uint32_t *codes,
-                               uint32_t *valid, hipStream_t s) {
-    const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
-    if (nt == 0) return hipSuccess;
-    k_fasta_encode<<<(unsigned)nt, NT, 0, s>>>(fa, n, tile_prev_nl, first_hdr, tile_off, codes, valid);
-    return hipGetLastError();
-}
-
+#include "fk_parse.inc"
 #include "fk_signature.inc"
 #include "fk_records.inc"
 #include "fk_partition.inc"
