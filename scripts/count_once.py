@@ -1,4 +1,5 @@
-import os, sys, time
+"""One counter, three counts of the bench workload; prints the stage split (for profilers)."""
+import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa
 import fastkmer_amd as fk
@@ -7,4 +8,5 @@ kc.synth_device(1_000_000_000 // 114, 100, 100_000_000, seed=0x5EED)
 for i in range(3):
     kc.finish()
 st = kc.stats()
-print(f"count {st['ms_count']:.2f} ms  buckets {st['buckets']} F {st['fine_bits']} oversize {st['oversize_buckets']} distinct {st['distinct']}")
+print(f"count {st['ms_count']:.2f} ms  partition {st['ms_partition']:.2f}  buckets {st['buckets']} F {st['fine_bits']} "
+      f"oversize {st['oversize_buckets']} kmers {st['kmers']} distinct {st['distinct']}", flush=True)
