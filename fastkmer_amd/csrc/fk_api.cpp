@@ -109,6 +109,7 @@ struct fk_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS: route every bucket through 5b
+    uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: cap/4)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
 
     // input
@@ -254,6 +255,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->fm = make_fastmod((uint32_t)c->Bc);
     const char *dbg = getenv("FASTKMER_DEBUG_LARGE_BUCKETS");
     c->force_large = dbg && dbg[0] == '1';
+    const char *ct = getenv("FASTKMER_DEBUG_CELL_TARGET");
+    c->cell_target = ct ? (uint32_t)atoi(ct) : 0u;
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
     if (cfg->device >= 0) {
@@ -521,8 +524,9 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // cell bits: the largest bin's cells average cap/4 keys (a bucket groups a
     // few cells; runs of one chunk's keys per cell stay long enough to be
     // written as whole lines)
+    const uint64_t target = c->cell_target ? c->cell_target : cap / 4;
     int F = 1;
-    while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * (cap / 4) < max_bin_kmers) ++F;
+    while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
