@@ -82,6 +82,69 @@ void release(DevBuf &b) {
     b.bytes = 0;
 }
 
+// Record partition (fk_partition.inc): histogram -> scan -> scatter.
+struct PartBufs {
+    DevBuf H, K, Hs, Ks;                  // per-workgroup histograms (column-major) and their scans
+    DevBuf rec, kmer, off, cursor;        // per-part totals / offsets (device), cursor: global path only
+    uint32_t nparts = 0;
+    uint64_t nrec = 0;
+    bool global = false;                  // nparts > PART_MAX: global-atomic kernels
+    void release_all() {
+        for (DevBuf *b : {&H, &K, &Hs, &Ks, &rec, &kmer, &off, &cursor}) release(*b);
+    }
+};
+
+// Counts records and k-mers per part into pb.rec / pb.kmer (device) and keeps
+// what part_scatter needs.
+int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
+               ScanWorkspace &ws, hipStream_t s) {
+    pb.nparts = nparts;
+    pb.nrec = nrec;
+    pb.global = nparts > PART_MAX;
+    FK_TRY(ensure(pb.rec, ((uint64_t)nparts + 1) * 8));
+    FK_TRY(ensure(pb.kmer, ((uint64_t)nparts + 1) * 8));
+    FK_TRY(ensure(pb.off, ((uint64_t)nparts + 1) * 8));
+    if (pb.global) {
+        HIP_TRY(hipMemsetAsync(pb.rec.p, 0, ((uint64_t)nparts + 1) * 8, s));
+        HIP_TRY(hipMemsetAsync(pb.kmer.p, 0, ((uint64_t)nparts + 1) * 8, s));
+        HIP_TRY(launch_part_hist_global(W, recs, nrec, mode, G, nparts, pb.rec.as<uint64_t>(), pb.kmer.as<uint64_t>(),
+                                        s));
+        HIP_TRY(scan_excl_sum_u64(pb.rec.as<uint64_t>(), pb.off.as<uint64_t>(), nparts, pb.off.as<uint64_t>() + nparts,
+                                  ws, s));
+        return FK_OK;
+    }
+    const uint64_t n = (uint64_t)nparts * part_workgroups(nrec);
+    FK_TRY(ensure(pb.H, n * 4));
+    FK_TRY(ensure(pb.K, n * 4));
+    FK_TRY(ensure(pb.Hs, (n + 1) * 8));
+    FK_TRY(ensure(pb.Ks, (n + 1) * 8));
+    if (n) {
+        HIP_TRY(launch_part_hist(W, recs, nrec, mode, G, nparts, pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), s));
+        HIP_TRY(scan_excl_sum_u32_to_u64(pb.H.as<uint32_t>(), pb.Hs.as<uint64_t>(), n, pb.Hs.as<uint64_t>() + n, ws, s));
+        HIP_TRY(scan_excl_sum_u32_to_u64(pb.K.as<uint32_t>(), pb.Ks.as<uint64_t>(), n, pb.Ks.as<uint64_t>() + n, ws, s));
+        HIP_TRY(launch_part_totals(pb.Hs.as<uint64_t>(), pb.Ks.as<uint64_t>(), nparts, nrec, pb.rec.as<uint64_t>(),
+                                   pb.kmer.as<uint64_t>(), pb.off.as<uint64_t>(), s));
+    } else {
+        HIP_TRY(hipMemsetAsync(pb.rec.p, 0, ((uint64_t)nparts + 1) * 8, s));
+        HIP_TRY(hipMemsetAsync(pb.kmer.p, 0, ((uint64_t)nparts + 1) * 8, s));
+        HIP_TRY(hipMemsetAsync(pb.off.p, 0, ((uint64_t)nparts + 1) * 8, s));
+    }
+    return FK_OK;
+}
+
+// Writes the records grouped by part (parts in order) into out.
+int part_scatter(PartBufs &pb, int W, const uint64_t *recs, int mode, uint32_t G, uint64_t *out, hipStream_t s) {
+    if (pb.global) {
+        FK_TRY(ensure(pb.cursor, ((uint64_t)pb.nparts + 1) * 8));
+        HIP_TRY(hipMemsetAsync(pb.cursor.p, 0, ((uint64_t)pb.nparts + 1) * 8, s));
+        HIP_TRY(launch_part_scatter_global(W, recs, pb.nrec, mode, G, pb.nparts, pb.off.as<uint64_t>(), pb.cursor.as<uint64_t>(),
+                                           out, s));
+        return FK_OK;
+    }
+    HIP_TRY(launch_part_scatter(W, recs, pb.nrec, mode, G, pb.nparts, pb.Hs.as<uint64_t>(), out, s));
+    return FK_OK;
+}
+
 int32_t clamp_bins(int32_t m, int32_t B) {
     // test/package.scala:32: Math.min(Math.pow(4, m), max_b).toInt
     double p = 1.0;
@@ -125,10 +188,10 @@ struct fk_ctx {
     uint64_t nrec = 0, nkmers = 0;
     bool mapped = false;
     // destination partition (n_ranks > 1)
-    DevBuf dest_rec, dest_kmer, dest_off, dest_cursor;
     std::vector<uint64_t> send_counts;
     // reduce
-    DevBuf part_rec, part_kmer, part_off, part_cursor, precs, chunks, bin_chunk_begin;
+    PartBufs dest, part;  // record partition by destination rank (fk_map) / by local bin (fk_reduce)
+    DevBuf precs, chunks, bin_chunk_begin;
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc;
@@ -293,14 +356,15 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
-                      &c->dest_rec, &c->dest_kmer, &c->dest_off, &c->dest_cursor, &c->part_rec, &c->part_kmer,
-                      &c->part_off, &c->part_cursor, &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk,
+                      &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
                       &c->tcounts};
     for (DevBuf *b : bufs) release(*b);
+    c->dest.release_all();
+    c->part.release_all();
     if (c->ws.ptr) (void)hipFree(c->ws.ptr);
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -471,13 +535,8 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (c->G == 1) {
         c->send_counts[0] = c->nrec;
     } else if (c->nrec) {
-        FK_TRY(ensure(c->dest_rec, c->G * 8));
-        FK_TRY(ensure(c->dest_kmer, c->G * 8));
-        HIP_TRY(hipMemsetAsync(c->dest_rec.p, 0, c->G * 8, s));
-        HIP_TRY(hipMemsetAsync(c->dest_kmer.p, 0, c->G * 8, s));
-        HIP_TRY(launch_part_hist(c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, c->G,
-                                 c->dest_rec.as<uint64_t>(), c->dest_kmer.as<uint64_t>(), s));
-        HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest_rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
+        FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, c->G, c->ws, s));
+        HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest.rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
     if (send_counts)
@@ -498,15 +557,7 @@ FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
     if (c->G == 1) {
         HIP_TRY(hipMemcpyAsync(d_send, c->records.p, c->nrec * c->W * 8, hipMemcpyDeviceToDevice, s));
     } else {
-        std::vector<uint64_t> off(c->G, 0);
-        for (uint32_t r = 1; r < c->G; ++r) off[r] = off[r - 1] + c->send_counts[r - 1];
-        FK_TRY(ensure(c->dest_off, c->G * 8));
-        FK_TRY(ensure(c->dest_cursor, c->G * 8));
-        HIP_TRY(hipMemcpyAsync(c->dest_off.p, off.data(), c->G * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(c->dest_cursor.p, 0, c->G * 8, s));
-        HIP_TRY(launch_part_scatter(c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, c->G,
-                                    c->dest_off.as<uint64_t>(), c->dest_cursor.as<unsigned long long>(),
-                                    (uint64_t *)d_send, s));
+        FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, (uint64_t *)d_send, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
     c->stats.ms_total += now_ms() - t0;
@@ -655,19 +706,12 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     hipStream_t s = c->stream;
     c->have_result = false;
     const uint32_t nlb = c->nlb;
-    FK_TRY(ensure(c->part_rec, ((uint64_t)nlb + 1) * 8));
-    FK_TRY(ensure(c->part_kmer, ((uint64_t)nlb + 1) * 8));
-    FK_TRY(ensure(c->part_off, ((uint64_t)nlb + 1) * 8));
-    FK_TRY(ensure(c->part_cursor, ((uint64_t)nlb + 1) * 8));
     HIP_TRY(hipEventRecord(c->ev[4], s));
-    HIP_TRY(hipMemsetAsync(c->part_rec.p, 0, ((uint64_t)nlb + 1) * 8, s));
-    HIP_TRY(hipMemsetAsync(c->part_kmer.p, 0, ((uint64_t)nlb + 1) * 8, s));
-    HIP_TRY(launch_part_hist(c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, nlb, c->part_rec.as<uint64_t>(),
-                             c->part_kmer.as<uint64_t>(), s));
+    FK_TRY(part_count(c->part, c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, nlb, c->ws, s));
     std::vector<uint64_t> brec(nlb), bkm(nlb);
     if (nlb) {
-        HIP_TRY(hipMemcpyAsync(brec.data(), c->part_rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(bkm.data(), c->part_kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(brec.data(), c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(bkm.data(), c->part.kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
     // record offsets per local bin and chunk table (chunks never span bins)
@@ -697,12 +741,9 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     FK_TRY(ensure(c->precs, nrecv * c->W * 8));
     FK_TRY(ensure(c->chunks, nchunks * sizeof(Chunk)));
     FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)nlb + 1) * 4));
-    HIP_TRY(hipMemcpyAsync(c->part_off.p, roff.data(), (nlb + 1) * 8, hipMemcpyHostToDevice, s));
     if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), (nlb + 1) * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(c->part_cursor.p, 0, ((uint64_t)nlb + 1) * 8, s));
-    HIP_TRY(launch_part_scatter(c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, nlb, c->part_off.as<uint64_t>(),
-                                c->part_cursor.as<unsigned long long>(), c->precs.as<uint64_t>(), s));
+    FK_TRY(part_scatter(c->part, c->W, (const uint64_t *)d_recv, 1, c->G, c->precs.as<uint64_t>(), s));
     HIP_TRY(hipEventRecord(c->ev[5], s));
     HIP_TRY(hipEventRecord(c->ev[6], s));
     if (c->cfg.use_ht)

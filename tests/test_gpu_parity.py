@@ -191,6 +191,15 @@ def test_large_bucket_path_vs_oracle(monkeypatch):
         assert_same_as_oracle(kc, ref)
 
 
+@pytest.mark.parametrize("use_ht", [False, True])
+def test_many_bins_global_partition_vs_oracle(use_ht):
+    # b = 20000 bins > PART_MAX: the record partition takes its global-atomic path
+    fasta = fk.synth_fasta(8000, 100, 200_000, seed=31)
+    kc = run_counter(fasta, 24, 9, 3, 20000, use_ht)
+    ref = oracle.OracleResult(fasta, 24, 9, 20000)
+    assert_same_as_oracle(kc, ref, ordered=not use_ht)
+
+
 def test_skewed_repeats_vs_oracle():
     # one k-mer repeated ~100k times, poly-A/poly-C blocks: single cells far above the LDS capacity
     fasta = (b">a\n" + b"A" * 100_000 + b"\n>b\n" + b"AC" * 60_000 + b"\n>c\n" + b"ACGTTGCA" * 20_000 + b"\n")
