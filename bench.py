@@ -158,8 +158,8 @@ def main() -> None:
                        "k": K, "m": M, "x": X, "B": B, "useHT": 0, "fasta_bytes_per_gpu": fasta_bytes,
                        "bases_per_gpu": bases_per_rank, "parallelism": f"bins round-robin over {world} GPU(s)"},
             "roofline": {"bound": "hbm",
-                         "kernel": "encode+signature stage: k_fasta_marks + k_fasta_count + k_fasta_encode + "
-                                   "k_superkmers (+ their scans/memsets)",
+                         "kernel": "encode+signature stage: k_fasta_parse + k_superkmers (+ their memsets and "
+                                   "the per-tile k-mer count scan)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": load_traffic(),
                          "bytes_alg_per_launch": fasta_bytes, "ms_per_launch": t_es * 1e3},
