@@ -76,6 +76,8 @@ def main() -> None:
     ap.add_argument("--bytes-per-gpu", type=int, default=FASTA_BYTES_PER_GPU)
     ap.add_argument("--cpu-sample-bytes", type=int, default=64_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--balance", action="store_true",
+                    help="size-aware bin placement (reference useCustomPartitioner=1) instead of bin %% N")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo stages records through host memory "
                          "(rehearsal of N > 1 with ranks sharing a GPU)")
@@ -103,7 +105,7 @@ def main() -> None:
 
     def step():
         if distributed:
-            count_distributed(kc, device=dev)
+            count_distributed(kc, device=dev, balance=args.balance)
         else:
             kc.finish()
 
@@ -156,7 +158,8 @@ def main() -> None:
             "data": "synthetic (device-generated 100 bp reads, 100 Mbp virtual genome, 0.2% subst, 0.05% N)",
             "config": {"workload": "BASELINE configs[1]: k=28 m=10 x=3 B=2048, 1 GB synthetic 100 bp reads per GPU",
                        "k": K, "m": M, "x": X, "B": B, "useHT": 0, "fasta_bytes_per_gpu": fasta_bytes,
-                       "bases_per_gpu": bases_per_rank, "parallelism": f"bins round-robin over {world} GPU(s)"},
+                       "bases_per_gpu": bases_per_rank, "parallelism": (f"bins placed by size (LPT) over {world} GPU(s)" if args.balance and distributed
+                                           else f"bins round-robin over {world} GPU(s)")},
             "roofline": {"bound": "hbm",
                          "kernel": "encode+signature stage: k_fasta_parse + k_superkmers (+ their memsets and "
                                    "the per-tile k-mer count scan)",

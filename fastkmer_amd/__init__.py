@@ -109,6 +109,9 @@ def lib():
         "fk_get_bin": (ctypes.c_int, [P, I32, P, P, SZ, ctypes.POINTER(SZ)]),
         "fk_write_bins": (ctypes.c_int, [P, ctypes.c_char_p]),
         "fk_get_stats": (ctypes.c_int, [P, ctypes.POINTER(fk_stats)]),
+        "fk_map_bin_kmers": (ctypes.c_int, [P, P]),
+        "fk_lpt_owners": (ctypes.c_int, [P, I32, I32, P]),
+        "fk_set_bin_owners": (ctypes.c_int, [P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -261,6 +264,23 @@ class KmerCounter:
         _check(lib().fk_map(self._h, counts))
         return list(counts)
 
+    def map_bin_kmers(self) -> np.ndarray:
+        """After map(): k-mers per bin (all b bins) of this rank's records."""
+        out = np.zeros(self.num_bins, dtype=np.uint64)
+        _check(lib().fk_map_bin_kmers(self._h, out.ctypes.data))
+        return out
+
+    def set_bin_owners(self, owner) -> list[int]:
+        """Install a bin -> rank placement (identical on every rank); returns the
+        send counts of the mapped records under it."""
+        own = np.ascontiguousarray(owner, dtype=np.int32)
+        if own.shape != (self.num_bins,):
+            raise ValueError(f"owner table needs {self.num_bins} entries")
+        counts = (ctypes.c_uint64 * self.n_ranks)()
+        _check(lib().fk_set_bin_owners(self._h, own.ctypes.data, counts))
+        self._sizes = None
+        return list(counts)
+
     def map_emit(self, dst_ptr: int, cap_records: int) -> None:
         _check(lib().fk_map_emit(self._h, ctypes.c_void_p(dst_ptr), cap_records))
 
@@ -309,6 +329,15 @@ class KmerCounter:
         st = fk_stats()
         _check(lib().fk_get_stats(self._h, ctypes.byref(st)))
         return {n: getattr(st, n) for n, _ in fk_stats._fields_}
+
+
+def lpt_owners(sizes, n_ranks: int) -> np.ndarray:
+    """MultiprocessorSchedulingPartitioner.solve (MultiprocessorSchedulingPartitioner.scala:35-69):
+    bins largest first onto the least loaded rank; bins of size 0 stay at bin % n_ranks."""
+    sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+    owner = np.zeros(len(sz), dtype=np.int32)
+    _check(lib().fk_lpt_owners(sz.ctypes.data, len(sz), n_ranks, owner.ctypes.data))
+    return owner
 
 
 def execute_job(configuration: TestConfiguration) -> KmerCounter:

@@ -96,8 +96,8 @@ struct PartBufs {
 
 // Counts records and k-mers per part into pb.rec / pb.kmer (device) and keeps
 // what part_scatter needs.
-int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
-               ScanWorkspace &ws, hipStream_t s) {
+int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mode, uint32_t G, const uint32_t *table,
+               uint32_t nparts, ScanWorkspace &ws, hipStream_t s) {
     pb.nparts = nparts;
     pb.nrec = nrec;
     pb.global = nparts > PART_MAX;
@@ -107,8 +107,8 @@ int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mod
     if (pb.global) {
         HIP_TRY(hipMemsetAsync(pb.rec.p, 0, ((uint64_t)nparts + 1) * 8, s));
         HIP_TRY(hipMemsetAsync(pb.kmer.p, 0, ((uint64_t)nparts + 1) * 8, s));
-        HIP_TRY(launch_part_hist_global(W, recs, nrec, mode, G, nparts, pb.rec.as<uint64_t>(), pb.kmer.as<uint64_t>(),
-                                        s));
+        HIP_TRY(launch_part_hist_global(W, recs, nrec, mode, G, table, nparts, pb.rec.as<uint64_t>(),
+                                        pb.kmer.as<uint64_t>(), s));
         HIP_TRY(scan_excl_sum_u64(pb.rec.as<uint64_t>(), pb.off.as<uint64_t>(), nparts, pb.off.as<uint64_t>() + nparts,
                                   ws, s));
         return FK_OK;
@@ -119,7 +119,7 @@ int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mod
     FK_TRY(ensure(pb.Hs, (n + 1) * 8));
     FK_TRY(ensure(pb.Ks, (n + 1) * 8));
     if (n) {
-        HIP_TRY(launch_part_hist(W, recs, nrec, mode, G, nparts, pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), s));
+        HIP_TRY(launch_part_hist(W, recs, nrec, mode, G, table, nparts, pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), s));
         HIP_TRY(scan_excl_sum_u32_to_u64(pb.H.as<uint32_t>(), pb.Hs.as<uint64_t>(), n, pb.Hs.as<uint64_t>() + n, ws, s));
         HIP_TRY(scan_excl_sum_u32_to_u64(pb.K.as<uint32_t>(), pb.Ks.as<uint64_t>(), n, pb.Ks.as<uint64_t>() + n, ws, s));
         HIP_TRY(launch_part_totals(pb.Hs.as<uint64_t>(), pb.Ks.as<uint64_t>(), nparts, nrec, pb.rec.as<uint64_t>(),
@@ -133,15 +133,16 @@ int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mod
 }
 
 // Writes the records grouped by part (parts in order) into out.
-int part_scatter(PartBufs &pb, int W, const uint64_t *recs, int mode, uint32_t G, uint64_t *out, hipStream_t s) {
+int part_scatter(PartBufs &pb, int W, const uint64_t *recs, int mode, uint32_t G, const uint32_t *table, uint64_t *out,
+                 hipStream_t s) {
     if (pb.global) {
         FK_TRY(ensure(pb.cursor, ((uint64_t)pb.nparts + 1) * 8));
         HIP_TRY(hipMemsetAsync(pb.cursor.p, 0, ((uint64_t)pb.nparts + 1) * 8, s));
-        HIP_TRY(launch_part_scatter_global(W, recs, pb.nrec, mode, G, pb.nparts, pb.off.as<uint64_t>(), pb.cursor.as<uint64_t>(),
-                                           out, s));
+        HIP_TRY(launch_part_scatter_global(W, recs, pb.nrec, mode, G, table, pb.nparts, pb.off.as<uint64_t>(),
+                                           pb.cursor.as<uint64_t>(), out, s));
         return FK_OK;
     }
-    HIP_TRY(launch_part_scatter(W, recs, pb.nrec, mode, G, pb.nparts, pb.Hs.as<uint64_t>(), out, s));
+    HIP_TRY(launch_part_scatter(W, recs, pb.nrec, mode, G, table, pb.nparts, pb.Hs.as<uint64_t>(), out, s));
     return FK_OK;
 }
 
@@ -165,7 +166,12 @@ struct fk_ctx {
     fk_config cfg{};
     int32_t Bc = 0;    // b = min(4^m, B)
     uint32_t G = 1;    // ranks
-    uint32_t nlb = 0;  // local bins: b = rank + G * lb
+    uint32_t nlb = 0;  // local bins: b = rank + G * lb (default placement) or lbin_bin[lb] (custom)
+    // size-aware placement (fk_set_bin_owners): bin -> rank, bin -> local index, local index -> bin
+    bool custom_owners = false;
+    std::vector<int32_t> h_owner, h_lbin_bin;
+    std::vector<uint32_t> h_bin_lbin;
+    DevBuf d_owner, d_local;  // REC_BIN_MASK + 1 entries each (~0u: no part), device copies of the above
     int W = 2, KW = 1;
     FastMod fm{};
     int device = 0;
@@ -190,7 +196,7 @@ struct fk_ctx {
     // destination partition (n_ranks > 1)
     std::vector<uint64_t> send_counts;
     // reduce
-    PartBufs dest, part;  // record partition by destination rank (fk_map) / by local bin (fk_reduce)
+    PartBufs dest, part, binhist;  // record partition by destination rank (fk_map) / by local bin (fk_reduce)
     DevBuf precs, chunks, bin_chunk_begin;
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
@@ -365,6 +371,9 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     for (DevBuf *b : bufs) release(*b);
     c->dest.release_all();
     c->part.release_all();
+    c->binhist.release_all();
+    release(c->d_owner);
+    release(c->d_local);
     if (c->ws.ptr) (void)hipFree(c->ws.ptr);
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -447,6 +456,12 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
         return 0.f;
     }
     return ms;
+}
+
+static const uint32_t *owner_table(const fk_ctx *c) { return c->custom_owners ? c->d_owner.as<uint32_t>() : nullptr; }
+static const uint32_t *local_table(const fk_ctx *c) { return c->custom_owners ? c->d_local.as<uint32_t>() : nullptr; }
+static int32_t global_bin(const fk_ctx *c, uint32_t lb) {
+    return c->custom_owners ? c->h_lbin_bin[lb] : (int32_t)(c->cfg.rank + lb * c->G);
 }
 
 FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
@@ -535,7 +550,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (c->G == 1) {
         c->send_counts[0] = c->nrec;
     } else if (c->nrec) {
-        FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, c->G, c->ws, s));
+        FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, owner_table(c), c->G, c->ws, s));
         HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest.rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
@@ -557,10 +572,88 @@ FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
     if (c->G == 1) {
         HIP_TRY(hipMemcpyAsync(d_send, c->records.p, c->nrec * c->W * 8, hipMemcpyDeviceToDevice, s));
     } else {
-        FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, (uint64_t *)d_send, s));
+        FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, owner_table(c), (uint64_t *)d_send, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
     c->stats.ms_total += now_ms() - t0;
+    return FK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// size-aware placement (MultiprocessorSchedulingPartitioner, SBKC:1023-1025)
+// ---------------------------------------------------------------------------
+
+FK_EXPORT int fk_map_bin_kmers(fk_ctx *c, uint64_t *kmers_per_bin) {
+    if (!c || !kmers_per_bin) return set_err(FK_E_INVALID, "null argument");
+    if (!c->mapped) return set_err(FK_E_STATE, "fk_map_bin_kmers before fk_map");
+    hipStream_t s = c->stream;
+    FK_TRY(part_count(c->binhist, c->W, c->records.as<uint64_t>(), c->nrec, 1, 1, nullptr, (uint32_t)c->Bc, c->ws, s));
+    HIP_TRY(hipMemcpyAsync(kmers_per_bin, c->binhist.kmer.p, (uint64_t)c->Bc * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FK_OK;
+}
+
+FK_EXPORT int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks, int32_t *owner) {
+    if (!sizes || !owner || nbins < 0 || nranks < 1) return set_err(FK_E_INVALID, "bad argument");
+    // largest first onto the least loaded rank (ties: lowest bin, lowest rank); bins of
+    // size 0 were not seen by the estimate and keep the hash placement bin % nranks
+    std::vector<int32_t> order;
+    for (int32_t b = 0; b < nbins; ++b) {
+        if (sizes[b])
+            order.push_back(b);
+        else
+            owner[b] = b % nranks;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return sizes[a] > sizes[b]; });
+    std::vector<uint64_t> load(nranks, 0);
+    for (int32_t b : order) {
+        int32_t r = 0;
+        for (int32_t q = 1; q < nranks; ++q)
+            if (load[q] < load[r]) r = q;
+        owner[b] = r;
+        load[r] += sizes[b];
+    }
+    return FK_OK;
+}
+
+FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_counts) {
+    if (!c || !owner) return set_err(FK_E_INVALID, "null argument");
+    for (int32_t b = 0; b < c->Bc; ++b)
+        if (owner[b] < 0 || (uint32_t)owner[b] >= c->G)
+            return set_err(FK_E_INVALID, "owner[%d] = %d is not a rank of %u", b, owner[b], c->G);
+    hipStream_t s = c->stream;
+    c->h_owner.assign(owner, owner + c->Bc);
+    c->h_bin_lbin.assign(c->Bc, ~0u);
+    c->h_lbin_bin.clear();
+    for (int32_t b = 0; b < c->Bc; ++b)
+        if (owner[b] == c->cfg.rank) {
+            c->h_bin_lbin[b] = (uint32_t)c->h_lbin_bin.size();
+            c->h_lbin_bin.push_back(b);
+        }
+    c->nlb = (uint32_t)c->h_lbin_bin.size();
+    // device maps over every value the 22-bit record bin field can hold
+    const uint64_t ntab = (uint64_t)REC_BIN_MASK + 1;
+    FK_TRY(ensure(c->d_owner, ntab * 4));
+    FK_TRY(ensure(c->d_local, ntab * 4));
+    HIP_TRY(hipMemsetAsync(c->d_owner.p, 0xff, ntab * 4, s));
+    HIP_TRY(hipMemsetAsync(c->d_local.p, 0xff, ntab * 4, s));
+    HIP_TRY(hipMemcpyAsync(c->d_owner.p, c->h_owner.data(), (uint64_t)c->Bc * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->d_local.p, c->h_bin_lbin.data(), (uint64_t)c->Bc * 4, hipMemcpyHostToDevice, s));
+    c->custom_owners = true;
+    c->have_result = false;
+    if (c->mapped) {  // the destinations of the mapped records changed
+        c->send_counts.assign(c->G, 0);
+        if (c->G == 1) {
+            c->send_counts[0] = c->nrec;
+        } else if (c->nrec) {
+            FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, owner_table(c), c->G, c->ws,
+                              s));
+            HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest.rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    if (send_counts)
+        for (uint32_t r = 0; r < c->G; ++r) send_counts[r] = c->mapped ? c->send_counts[r] : 0;
     return FK_OK;
 }
 
@@ -707,7 +800,7 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     c->have_result = false;
     const uint32_t nlb = c->nlb;
     HIP_TRY(hipEventRecord(c->ev[4], s));
-    FK_TRY(part_count(c->part, c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, nlb, c->ws, s));
+    FK_TRY(part_count(c->part, c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, local_table(c), nlb, c->ws, s));
     std::vector<uint64_t> brec(nlb), bkm(nlb);
     if (nlb) {
         HIP_TRY(hipMemcpyAsync(brec.data(), c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
@@ -743,7 +836,7 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)nlb + 1) * 4));
     if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), (nlb + 1) * 4, hipMemcpyHostToDevice, s));
-    FK_TRY(part_scatter(c->part, c->W, (const uint64_t *)d_recv, 1, c->G, c->precs.as<uint64_t>(), s));
+    FK_TRY(part_scatter(c->part, c->W, (const uint64_t *)d_recv, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
     HIP_TRY(hipEventRecord(c->ev[5], s));
     HIP_TRY(hipEventRecord(c->ev[6], s));
     if (c->cfg.use_ht)
@@ -774,14 +867,18 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
 // results
 // ---------------------------------------------------------------------------
 
-static bool owns(const fk_ctx *c, int32_t b) { return b >= 0 && b < c->Bc && (uint32_t)b % c->G == (uint32_t)c->cfg.rank; }
+static bool owns(const fk_ctx *c, int32_t b) {
+    if (b < 0 || b >= c->Bc) return false;
+    return c->custom_owners ? c->h_owner[b] == c->cfg.rank : (uint32_t)b % c->G == (uint32_t)c->cfg.rank;
+}
+static uint32_t local_bin(const fk_ctx *c, int32_t b) { return c->custom_owners ? c->h_bin_lbin[b] : (uint32_t)b / c->G; }
 
 FK_EXPORT int fk_bin_sizes(fk_ctx *c, uint64_t *out) {
     if (!c || !out) return set_err(FK_E_INVALID, "null argument");
     if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
     for (int32_t b = 0; b < c->Bc; ++b) {
         if (owns(c, b)) {
-            const uint32_t lb = (uint32_t)b / c->G;
+            const uint32_t lb = local_bin(c, b);
             out[b] = c->h_bin_off[lb + 1] - c->h_bin_off[lb];
         } else {
             out[b] = 0;
@@ -798,7 +895,7 @@ FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *count
         *n = 0;
         return FK_OK;
     }
-    const uint32_t lb = (uint32_t)bin / c->G;
+    const uint32_t lb = local_bin(c, bin);
     const uint64_t b0 = c->h_bin_off[lb], cnt = c->h_bin_off[lb + 1] - b0;
     *n = (size_t)cnt;
     if (cnt == 0) return FK_OK;
@@ -871,7 +968,7 @@ FK_EXPORT int fk_write_bins(fk_ctx *c, const char *out_dir) {
             for (uint32_t lb = t; lb < c->nlb; lb += nth) {
                 const uint64_t b0 = c->h_bin_off[lb], b1 = c->h_bin_off[lb + 1];
                 if (b1 == b0) continue;
-                const uint32_t bin = (uint32_t)c->cfg.rank + lb * c->G;
+                const uint32_t bin = (uint32_t)global_bin(c, lb);
                 buf.resize((b1 - b0) * (size_t)(k + 13) + 8);
                 size_t p = 0;
                 for (uint64_t i = b0; i < b1; ++i) {

@@ -68,17 +68,20 @@ hipError_t launch_fill_u64(uint64_t *p, uint64_t n, uint64_t v, hipStream_t s);
 constexpr uint32_t PART_CHUNK = 16384;  // records per partition workgroup
 constexpr uint32_t PART_MAX = 12288;    // parts per partition pass (LDS histogram)
 uint32_t part_workgroups(uint64_t nrec);
-hipError_t launch_part_hist(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
-                            uint32_t *H, uint32_t *K, hipStream_t s);
+// table: optional bin -> part map (size-aware placement); null: the formula
+hipError_t launch_part_hist(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, const uint32_t *table,
+                            uint32_t nparts, uint32_t *H, uint32_t *K, hipStream_t s);
 hipError_t launch_part_totals(const uint64_t *Hs, const uint64_t *Ks, uint32_t nparts, uint64_t nrec,
                               uint64_t *part_rec, uint64_t *part_kmer, uint64_t *part_off, hipStream_t s);
-hipError_t launch_part_scatter(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
-                               const uint64_t *Hs, uint64_t *out, hipStream_t s);
+hipError_t launch_part_scatter(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, const uint32_t *table,
+                               uint32_t nparts, const uint64_t *Hs, uint64_t *out, hipStream_t s);
 // nparts > PART_MAX: totals by global atomics (part_rec/part_kmer zeroed), scatter by per-part cursors
-hipError_t launch_part_hist_global(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
-                                   uint64_t *part_rec, uint64_t *part_kmer, hipStream_t s);
-hipError_t launch_part_scatter_global(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, uint32_t nparts,
-                                      const uint64_t *part_off, uint64_t *part_cursor, uint64_t *out, hipStream_t s);
+hipError_t launch_part_hist_global(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G,
+                                   const uint32_t *table, uint32_t nparts, uint64_t *part_rec, uint64_t *part_kmer,
+                                   hipStream_t s);
+hipError_t launch_part_scatter_global(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G,
+                                      const uint32_t *table, uint32_t nparts, const uint64_t *part_off,
+                                      uint64_t *part_cursor, uint64_t *out, hipStream_t s);
 
 // ---- sorted count
 hipError_t launch_expand_hist(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,

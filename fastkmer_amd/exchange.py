@@ -16,7 +16,7 @@ import torch.distributed as dist
 
 
 def owner_of_bin(b: int, world: int) -> int:
-    """Rank that counts bin b (round-robin ownership)."""
+    """Rank that counts bin b under the default placement (round-robin)."""
     return b % world
 
 
@@ -48,14 +48,31 @@ def exchange_records(send: torch.Tensor, send_counts: list[int], record_bytes: i
     return (recv.to(dev) if host else recv), recv_counts
 
 
-def count_distributed(counter, group=None, device=None):
+def balanced_owners(counter, group=None, device=None):
+    """Size-aware placement (useCustomPartitioner, SBKC:1023-1025): exact k-mers
+    per bin summed over the ranks (one all-reduce of b counts), then LPT
+    (fastkmer_amd.lpt_owners).  Call after counter.map(); returns the owner table."""
+    import fastkmer_amd as fk
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    host = dist.get_backend(group) == "gloo"
+    sizes = torch.from_numpy(counter.map_bin_kmers().astype("int64"))
+    sizes = sizes if host else sizes.to(dev)
+    dist.all_reduce(sizes, op=dist.ReduceOp.SUM, group=group)
+    return fk.lpt_owners(sizes.cpu().numpy().astype("uint64"), dist.get_world_size(group))
+
+
+def count_distributed(counter, group=None, device=None, balance: bool = False):
     """map -> all-to-all -> reduce for one rank of a multi-GPU job.
 
     ``counter`` is a fastkmer_amd.KmerCounter created with n_ranks/rank and
-    already holding its input shard.  Returns the number of records received.
+    already holding its input shard.  balance=True places bins by size
+    (balanced_owners) instead of bin % world.  Returns the number of records
+    received.
     """
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     send_counts = counter.map()
+    if balance:
+        send_counts = counter.set_bin_owners(balanced_owners(counter, group, dev))
     total = sum(send_counts)
     rb = counter.record_bytes
     send = torch.empty(max(total, 1) * rb, dtype=torch.uint8, device=dev)
@@ -89,7 +106,7 @@ def execute_job_distributed(configuration, group=None, device=None):
                         configuration.useHT, configuration.sequenceType, n_ranks=world, rank=rank,
                         device=dev.index if dev.index is not None else -1)
     kc.ingest(piece)
-    count_distributed(kc, group=group, device=dev)
+    count_distributed(kc, group=group, device=dev, balance=configuration.useCustomPartitioner)
     if configuration.write:
         kc.write_bins(configuration.outputDir)
     return kc

@@ -121,6 +121,19 @@ int fk_reduce(fk_ctx *ctx, const void *d_recv, uint64_t n_records);
 /* Single rank: fk_map + fk_reduce on the local records. */
 int fk_finish(fk_ctx *ctx);
 
+/* Size-aware bin placement, the MultiprocessorSchedulingPartitioner of the
+ * reference (SBKC:1023-1025, MultiprocessorSchedulingPartitioner.scala:35-69)
+ * with exact sizes instead of a 1% sample.  Default placement: bin % n_ranks.
+ *   fk_map_bin_kmers: after fk_map, the k-mers per bin of this rank's records
+ *     (all b bins); sum them over the ranks (e.g. an all-reduce),
+ *   fk_lpt_owners: largest bin first onto the least loaded rank (host only;
+ *     bins of size 0 keep bin % n_ranks),
+ *   fk_set_bin_owners: install owner[b] (the same table on every rank) before
+ *     fk_map_emit / fk_reduce; recomputes send_counts when already mapped. */
+int fk_map_bin_kmers(fk_ctx *ctx, uint64_t *kmers_per_bin);
+int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks, int32_t *owner);
+int fk_set_bin_owners(fk_ctx *ctx, const int32_t *owner, uint64_t *send_counts);
+
 /* ---- results (device resident; copied out on request) ------------------ */
 
 int32_t fk_num_bins(const fk_ctx *ctx); /* b = min(4^m, B) */

@@ -6,6 +6,7 @@ import ctypes
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 import fastkmer_amd as fk
@@ -112,3 +113,32 @@ def test_cli_usage_errors():
     r = subprocess.run([fk_cli, "28", "16", "3", "2048", "0", "0", "in", "out", "p", "0", "0", "0"],
                        capture_output=True)
     assert r.returncode == 1 and b"invalid configuration" in r.stderr
+
+
+def _lpt_reference(sizes, n):
+    # MultiprocessorSchedulingPartitioner.solve (MultiprocessorSchedulingPartitioner.scala:35-69) on
+    # the bins seen by the estimate, sorted by size descending (SBKC:1024); unseen bins hash to b % n
+    # (getPartition, :17-24).  The reference's final shuffle of partition ids only relabels ranks.
+    owner = [b % n for b in range(len(sizes))]
+    loads = [0] * n
+    for b in sorted((b for b in range(len(sizes)) if sizes[b]), key=lambda b: -sizes[b]):
+        r = min(range(n), key=lambda q: loads[q])
+        owner[b] = r
+        loads[r] += sizes[b]
+    return owner
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_lpt_owners_matches_reference_rule(n):
+    import random
+    rng = random.Random(n)
+    sizes = [rng.choice([0, 0, rng.randint(1, 10), rng.randint(1, 100_000)]) for _ in range(500)]
+    got = fk.lpt_owners(np.array(sizes, dtype=np.uint64), n)
+    assert list(got) == _lpt_reference(sizes, n)
+    loads = np.bincount(got, weights=sizes, minlength=n)
+    assert loads.max() - loads.min() <= max(sizes)
+
+
+def test_lpt_owners_validation():
+    with pytest.raises(fk.FastKmerError):
+        fk.lpt_owners(np.zeros(4, dtype=np.uint64), 0)

@@ -257,6 +257,54 @@ def test_multi_rank_in_one_process_matches_single():
                 assert np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
 
 
+@pytest.mark.parametrize("use_ht", [False, True])
+def test_size_aware_placement_in_one_process(use_ht):
+    # useCustomPartitioner: exact per-bin sizes summed over 3 ranks, LPT owners, records routed by the table
+    fasta = fk.synth_fasta(20_000, 100, 300_000, seed=19)
+    G, rec = 3, 114
+    shards = [fasta[r * rec * 7000:(r + 1) * rec * 7000] for r in range(G)]
+    ranks = [fk.KmerCounter(28, 10, 3, 2048, use_ht, 0, n_ranks=G, rank=r) for r in range(G)]
+    import torch
+    sizes = np.zeros(2048, dtype=np.uint64)
+    for r in range(G):
+        ranks[r].ingest(shards[r])
+        ranks[r].map()
+        sizes += ranks[r].map_bin_kmers()
+    owner = fk.lpt_owners(sizes, G)
+    loads = np.bincount(owner, weights=sizes.astype(np.float64), minlength=G)
+    assert loads.max() / loads.mean() < 1.01
+    sends = []
+    for r in range(G):
+        counts = ranks[r].set_bin_owners(owner)
+        buf = torch.empty(max(sum(counts), 1) * ranks[r].record_bytes, dtype=torch.uint8, device="cuda")
+        ranks[r].map_emit(buf.data_ptr(), max(sum(counts), 1))
+        torch.cuda.synchronize()
+        sends.append((buf, counts))
+    rb = ranks[0].record_bytes
+    for dst in range(G):
+        parts = []
+        for src in range(G):
+            buf, counts = sends[src]
+            off = sum(counts[:dst])
+            parts.append(buf[off * rb:(off + counts[dst]) * rb])
+        recv = torch.cat(parts)
+        ranks[dst].reduce(recv.data_ptr(), recv.numel() // rb)
+        torch.cuda.synchronize()
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    ref_sizes = ref.bin_sizes()
+    for dst in range(G):
+        got = ranks[dst].bin_sizes()
+        for b in range(ref.nbins):
+            assert got[b] == (ref_sizes[b] if owner[b] == dst else 0)
+            if owner[b] == dst and ref_sizes[b] and b % 97 == 0:
+                hi, lo, cnt = counter_arrays(ranks[dst], b)
+                rhi, rlo, rcnt = ref.bin_arrays(b)
+                if use_ht:
+                    order = np.argsort(lo)
+                    lo, cnt = lo[order], cnt[order]
+                assert np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
+
+
 def test_device_synth_matches_host():
     import torch
     kc = fk.KmerCounter(28, 10, 3, 2048)
