@@ -76,6 +76,9 @@ def main() -> None:
     ap.add_argument("--bytes-per-gpu", type=int, default=FASTA_BYTES_PER_GPU)
     ap.add_argument("--cpu-sample-bytes", type=int, default=64_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-input", action="store_true",
+                    help="PCIe-inclusive variant: the FASTA starts in pinned host memory and every step "
+                         "ingests it (H2D) before counting; reported as a separate metric, never as the headline")
     ap.add_argument("--balance", action="store_true",
                     help="size-aware bin placement (reference useCustomPartitioner=1) instead of bin %% N")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -102,8 +105,16 @@ def main() -> None:
     # per-rank shard of one synthetic read set (weak scaling: 1 GB per GPU)
     fasta_bytes = kc.synth_device(n_reads, READ_LEN, GENOME, seed=SEED, first_read=rank * n_reads)
     bases_per_rank = n_reads * READ_LEN
+    host_buf = None
+    if args.host_input:  # the same shard in pinned host memory, prepared outside the timed region
+        import numpy as np
+        host_buf = torch.empty(fasta_bytes, dtype=torch.uint8).pin_memory()
+        host_buf.copy_(torch.from_numpy(np.frombuffer(
+            fk.synth_fasta(n_reads, READ_LEN, GENOME, seed=SEED, first_read=rank * n_reads), dtype=np.uint8)))
 
     def step():
+        if host_buf is not None:
+            kc.ingest_ptr(host_buf.data_ptr(), fasta_bytes)
         if distributed:
             count_distributed(kc, device=dev, balance=args.balance)
         else:
@@ -143,8 +154,11 @@ def main() -> None:
         # time = every launch between FASTA and super-k-mer records (HIP events on the ctx stream)
         t_es = sum(stage_ms) / len(stage_ms) * 1e-3
         achieved = fasta_bytes / t_es
+        metric = "input bases/sec (whole node), k=28 short reads, 1/2/4/8 GPUs; counts bit-exact"
+        if args.host_input:
+            metric += " [PCIe-inclusive variant: FASTA in pinned host memory, H2D inside every step]"
         out = {
-            "metric": "input bases/sec (whole node), k=28 short reads, 1/2/4/8 GPUs; counts bit-exact",
+            "metric": metric,
             "value": value,
             "unit": "bases/s",
             "n_gpus": world,

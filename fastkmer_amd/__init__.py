@@ -245,6 +245,10 @@ class KmerCounter:
         self._keep = bytes(fasta)
         _check(lib().fk_ingest(self._h, self._keep, len(self._keep), 1))
 
+    def ingest_ptr(self, ptr: int, n: int) -> None:
+        """Append n host bytes at ptr (pinned memory is copied by DMA directly)."""
+        _check(lib().fk_ingest(self._h, ctypes.cast(ptr, ctypes.c_char_p), n, 1))
+
     def ingest_device(self, ptr: int, n: int) -> None:
         _check(lib().fk_ingest_device(self._h, ctypes.c_void_p(ptr), n, 1))
 

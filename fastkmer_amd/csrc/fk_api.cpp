@@ -182,7 +182,10 @@ struct fk_ctx {
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
 
     // input
-    std::vector<uint8_t> host_in;
+    // host ingest: bytes are streamed to fasta_own (appended until the next fk_map)
+    bool ingest_fresh = true;        // the next fk_ingest starts a new input
+    void *pinned[2] = {nullptr, nullptr};  // staging for pageable sources
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
     const uint8_t *d_fasta = nullptr;
     uint64_t n_fasta = 0;
     DevBuf fasta_own;
@@ -369,6 +372,10 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
                       &c->tcounts};
     for (DevBuf *b : bufs) release(*b);
+    for (int i = 0; i < 2; ++i) {
+        if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
+        if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
+    }
     c->dest.release_all();
     c->part.release_all();
     c->binhist.release_all();
@@ -402,14 +409,57 @@ static void reset_results(fk_ctx *c) {
     c->h_bin_off.clear();
 }
 
+constexpr size_t PIN_CHUNK = 64ull << 20;  // pinned staging buffer (x2) for pageable sources
+
+// Appends host bytes to the device input.  Pinned sources are copied by DMA
+// directly; pageable ones through two pinned staging buffers, the memcpy of
+// one chunk overlapping the DMA of the previous one.  Returns after the
+// source has been read.
 FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     (void)last;
     if (!c || (!fasta && n)) return set_err(FK_E_INVALID, "null argument");
     if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>())
         return set_err(FK_E_STATE, "fk_ingest after fk_ingest_device on the same job");
-    c->host_in.insert(c->host_in.end(), fasta, fasta + n);
-    c->d_fasta = nullptr;
-    c->n_fasta = c->host_in.size();
+    hipStream_t s = c->stream;
+    if (c->ingest_fresh || !c->d_fasta) {
+        c->n_fasta = 0;
+        c->ingest_fresh = false;
+    }
+    const uint64_t have = c->n_fasta, need = have + n;
+    if (c->fasta_own.bytes < need) {  // grow, keeping what was ingested
+        DevBuf grown;
+        FK_TRY(ensure(grown, std::max<uint64_t>(need, 2 * (uint64_t)c->fasta_own.bytes)));
+        if (have) HIP_TRY(hipMemcpyAsync(grown.p, c->fasta_own.p, have, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        release(c->fasta_own);
+        c->fasta_own = grown;
+    }
+    uint8_t *dst = c->fasta_own.as<uint8_t>() + have;
+    hipPointerAttribute_t attr{};
+    const bool pinned = hipPointerGetAttributes(&attr, fasta) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    if (pinned || n == 0) {
+        if (n) HIP_TRY(hipMemcpyAsync(dst, fasta, n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        for (int i = 0; i < 2; ++i)
+            if (!c->pinned[i]) {
+                HIP_TRY(hipHostMalloc(&c->pinned[i], PIN_CHUNK, hipHostMallocDefault));
+                HIP_TRY(hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(c->pin_ev[i], s));
+            }
+        size_t off = 0;
+        for (int i = 0; off < n; ++i) {
+            const size_t len = std::min(PIN_CHUNK, n - off);
+            HIP_TRY(hipEventSynchronize(c->pin_ev[i & 1]));  // its previous DMA is done
+            memcpy(c->pinned[i & 1], fasta + off, len);
+            HIP_TRY(hipMemcpyAsync(dst + off, c->pinned[i & 1], len, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipEventRecord(c->pin_ev[i & 1], s));
+            off += len;
+        }
+    }
+    c->d_fasta = c->fasta_own.as<uint8_t>();
+    c->n_fasta = need;
     reset_results(c);
     return FK_OK;
 }
@@ -417,7 +467,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
 FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
     (void)last;
     if (!c || (!d && n)) return set_err(FK_E_INVALID, "null argument");
-    c->host_in.clear();
+    c->ingest_fresh = true;
     reset_results(c);
     if (((uintptr_t)d & 15) != 0) {
         FK_TRY(ensure(c->fasta_own, n));
@@ -438,7 +488,7 @@ FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_r
     FK_TRY(ensure(c->fasta_own, nb));
     HIP_TRY(launch_synth(c->fasta_own.as<uint8_t>(), nb, p, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->host_in.clear();
+    c->ingest_fresh = true;
     c->d_fasta = c->fasta_own.as<uint8_t>();
     c->n_fasta = nb;
     reset_results(c);
@@ -468,12 +518,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     const double t_start = now_ms();
     hipStream_t s = c->stream;
-    if (!c->host_in.empty() && !c->d_fasta) {
-        FK_TRY(ensure(c->fasta_own, c->host_in.size()));
-        HIP_TRY(hipMemcpyAsync(c->fasta_own.p, c->host_in.data(), c->host_in.size(), hipMemcpyHostToDevice, s));
-        c->d_fasta = c->fasta_own.as<uint8_t>();
-        c->n_fasta = c->host_in.size();
-    }
+    c->ingest_fresh = true;  // a later fk_ingest starts a new input
     const uint64_t n = c->d_fasta ? c->n_fasta : 0;
     reset_results(c);
     c->stats = fk_stats{};

@@ -305,6 +305,43 @@ def test_size_aware_placement_in_one_process(use_ht):
                 assert np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
 
 
+def test_chunked_and_pinned_ingest():
+    # fk_ingest appends: uneven chunks split inside records equal one call; a pinned
+    # source (DMA path) equals a pageable one (staged path)
+    import torch
+    fasta = fk.synth_fasta(20_000, 100, 300_000, seed=37)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    kc = fk.KmerCounter(28, 10, 3, 2048)
+    cuts = [0, 1, 777_777, 1_500_001, len(fasta)]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        kc.ingest(fasta[a:b])
+    kc.finish()
+    assert_same_as_oracle(kc, ref)
+    kc.finish()  # the same input again
+    assert_same_as_oracle(kc, ref)
+    pinned = torch.frombuffer(bytearray(fasta), dtype=torch.uint8).pin_memory()
+    kc.ingest_ptr(pinned.data_ptr(), pinned.numel())  # a new input after finish
+    kc.finish()
+    assert_same_as_oracle(kc, ref)
+
+
+def test_large_staged_ingest_matches_device_input():
+    # > 2 staging buffers (64 MB each) of pageable input == the same bytes generated on the device
+    n_reads = 1_500_000  # 171 MB
+    host = fk.synth_fasta(n_reads, 100, 5_000_000, seed=41)
+    a = fk.KmerCounter(25, 9, 3, 512)
+    a.ingest(host)
+    a.finish()
+    b = fk.KmerCounter(25, 9, 3, 512)
+    assert b.synth_device(n_reads, 100, 5_000_000, seed=41) == len(host)
+    b.finish()
+    assert np.array_equal(a.bin_sizes(), b.bin_sizes())
+    for bin_ in (0, 17, 511):
+        ka, ca = a.get_bin(bin_)
+        kb, cb = b.get_bin(bin_)
+        assert np.array_equal(ka, kb) and np.array_equal(ca, cb)
+
+
 def test_device_synth_matches_host():
     import torch
     kc = fk.KmerCounter(28, 10, 3, 2048)
