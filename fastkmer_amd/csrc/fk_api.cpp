@@ -968,70 +968,67 @@ static int mkdir_p(const std::string &path) {
     return 0;
 }
 
-// Kmer.toString (package.scala:416-454, 496-500) + "\t" + count + "\n"
-static size_t format_line(char *dst, uint64_t hi, uint64_t lo, uint32_t cnt, int k) {
-    static const char rep[4] = {'A', 'C', 'G', 'T'};
-    for (int t = 0; t < k; ++t) {
-        const int bit = 2 * (k - 1 - t);
-        const uint64_t v = bit >= 64 ? (hi >> (bit - 64)) : (lo >> bit);
-        dst[t] = rep[v & 3];
-    }
-    size_t p = (size_t)k;
-    dst[p++] = '\t';
-    char tmp[16];
-    int q = 0;
-    do {
-        tmp[q++] = (char)('0' + cnt % 10);
-        cnt /= 10;
-    } while (cnt);
-    while (q) dst[p++] = tmp[--q];
-    dst[p++] = '\n';
-    return p;
-}
-
+// Bin files (writers SBKC:550-606 / 715-734): the text is formatted on the
+// device (fk_format.inc), copied to the host once and written one file per bin.
 FK_EXPORT int fk_write_bins(fk_ctx *c, const char *out_dir) {
     if (!c || !out_dir) return set_err(FK_E_INVALID, "null argument");
     if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
     if (mkdir_p(out_dir) != 0) return set_err(FK_E_IO, "cannot create %s: %s", out_dir, strerror(errno));
+    hipStream_t s = c->stream;
     const uint64_t D = c->distinct;
-    std::vector<uint64_t> hk(D * c->KW);
-    std::vector<uint32_t> hc(D);
-    if (D) {
-        HIP_TRY(hipMemcpy(hk.data(), c->dense_keys.p, D * 8 * c->KW, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(hc.data(), c->dense_counts.p, D * 4, hipMemcpyDeviceToHost));
+    const uint32_t nlb = c->nlb;
+    const int eof = c->cfg.use_ht == 0;
+    if (D == 0) return FK_OK;  // no k-mers: no bin files
+    DevBuf len, off, bbytes, text;
+    struct Free {
+        DevBuf *b[4];
+        ~Free() {
+            for (DevBuf *x : b) release(*x);
+        }
+    } guard{{&len, &off, &bbytes, &text}};
+    FK_TRY(ensure(len, D * 4));
+    FK_TRY(ensure(off, (D + 1) * 8));
+    FK_TRY(ensure(bbytes, ((uint64_t)nlb + 1) * 8));
+    HIP_TRY(launch_format_lens(c->dense_counts.as<uint32_t>(), D, c->cfg.k, c->bin_off.as<uint64_t>(), nlb, eof,
+                               len.as<uint32_t>(), s));
+    HIP_TRY(scan_excl_sum_u32_to_u64(len.as<uint32_t>(), off.as<uint64_t>(), D, off.as<uint64_t>() + D, c->ws, s));
+    HIP_TRY(launch_gather_u64(off.as<uint64_t>(), c->bin_off.as<uint64_t>(), (uint64_t)nlb + 1,
+                              bbytes.as<uint64_t>(), s));
+    std::vector<uint64_t> bb(nlb + 1, 0);
+    HIP_TRY(hipMemcpyAsync(bb.data(), bbytes.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t T = bb[nlb];
+    FK_TRY(ensure(text, T + 16));
+    HIP_TRY(launch_format_lines(c->KW, c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(), D, c->cfg.k,
+                                off.as<uint64_t>(), text.as<uint8_t>(), s));
+    uint8_t *host = nullptr;
+    if (T) {
+        HIP_TRY(hipHostMalloc((void **)&host, T, hipHostMallocDefault));
+        const hipError_t e = hipMemcpyAsync(host, text.p, T, hipMemcpyDeviceToHost, s);
+        const hipError_t e2 = e == hipSuccess ? hipStreamSynchronize(s) : e;
+        if (e2 != hipSuccess) {
+            (void)hipHostFree(host);
+            return set_err(FK_E_DEVICE, "copying the bin text to the host: %s", hipGetErrorString(e2));
+        }
     }
-    const int k = c->cfg.k;
-    const int KW = c->KW;
-    const bool eof = c->cfg.use_ht == 0;
     const std::string dir(out_dir);
     const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<int> errs(nth, 0);
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nth; ++t) {
         th.emplace_back([&, t]() {
-            std::vector<char> buf;
-            for (uint32_t lb = t; lb < c->nlb; lb += nth) {
-                const uint64_t b0 = c->h_bin_off[lb], b1 = c->h_bin_off[lb + 1];
-                if (b1 == b0) continue;
-                const uint32_t bin = (uint32_t)global_bin(c, lb);
-                buf.resize((b1 - b0) * (size_t)(k + 13) + 8);
-                size_t p = 0;
-                for (uint64_t i = b0; i < b1; ++i) {
-                    const uint64_t hi = KW == 2 ? hk[2 * i] : 0, lo = KW == 2 ? hk[2 * i + 1] : hk[i];
-                    p += format_line(buf.data() + p, hi, lo, hc[i], k);
-                }
-                if (eof) {
-                    memcpy(buf.data() + p, "EOF", 3);
-                    p += 3;
-                }
-                const std::string path = dir + "/bin" + std::to_string(bin);
+            for (uint32_t lb = t; lb < nlb; lb += nth) {
+                if (c->h_bin_off[lb + 1] == c->h_bin_off[lb]) continue;  // empty bins have no file
+                const std::string path = dir + "/bin" + std::to_string(global_bin(c, lb));
                 FILE *f = fopen(path.c_str(), "wb");
-                if (!f || fwrite(buf.data(), 1, p, f) != p) errs[t] = 1;
-                if (f) fclose(f);
+                const size_t nb = (size_t)(bb[lb + 1] - bb[lb]);
+                if (!f || fwrite(host + bb[lb], 1, nb, f) != nb) errs[t] = 1;
+                if (f && fclose(f) != 0) errs[t] = 1;
             }
         });
     }
     for (auto &x : th) x.join();
+    if (host) (void)hipHostFree(host);
     for (int e : errs)
         if (e) return set_err(FK_E_IO, "writing bin files under %s failed", out_dir);
     return FK_OK;

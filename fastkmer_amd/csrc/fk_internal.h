@@ -124,4 +124,11 @@ hipError_t launch_ht_bin_offsets(const uint64_t *slot_scan, const uint64_t *tabl
 // ---- synthetic input
 hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);
 
+// ---- bin-file text (fk_format.inc) and a small gather: out[i] = src[idx[i]]
+hipError_t launch_format_lens(const uint32_t *counts, uint64_t n, int k, const uint64_t *bin_off, uint32_t nlb,
+                              int eof, uint32_t *len, hipStream_t s);
+hipError_t launch_format_lines(int KW, const uint64_t *keys, const uint32_t *counts, uint64_t n, int k,
+                               const uint64_t *off, uint8_t *out, hipStream_t s);
+hipError_t launch_gather_u64(const uint64_t *src, const uint64_t *idx, uint64_t n, uint64_t *out, hipStream_t s);
+
 }  // namespace fk
