@@ -179,6 +179,7 @@ struct fk_ctx {
     bool own_stream = false;
     bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS: route every bucket through 5b
     uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: cap/4)
+    int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
 
     // input
@@ -329,6 +330,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->force_large = dbg && dbg[0] == '1';
     const char *ct = getenv("FASTKMER_DEBUG_CELL_TARGET");
     c->cell_target = ct ? (uint32_t)atoi(ct) : 0u;
+    const char *sc = getenv("FASTKMER_DEBUG_SCATTER");
+    c->scatter_wc = (sc && sc[0]) ? atoi(sc) : 1;
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
     if (cfg->device >= 0) {
@@ -733,8 +736,22 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
                                c->cell_total.as<uint64_t>(), s));
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
                               c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
+    if (getenv("FASTKMER_DEBUG_CELL_SIZES")) {  // key-weighted histogram of log2(cell size), stderr
+        std::vector<uint64_t> ct(ncell_all);
+        HIP_TRY(hipMemcpyAsync(ct.data(), c->cell_total.p, ncell_all * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        uint64_t hk[64] = {0}, hc[64] = {0};
+        for (uint64_t v : ct) {
+            const int l = v ? 64 - __builtin_clzll(v) : 0;
+            hk[l] += v;
+            hc[l] += 1;
+        }
+        for (int l = 0; l < 40; ++l)
+            if (hc[l]) fprintf(stderr, "cells <2^%d: %llu cells %llu keys\n", l, (unsigned long long)hc[l], (unsigned long long)hk[l]);
+    }
     HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
-                                  c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(), s));
+                                  c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
+                                  max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
     HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
                                 cap - cap / 4, c->flags.as<uint32_t>(), s));
     HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), ncell_all,

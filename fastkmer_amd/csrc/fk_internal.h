@@ -89,7 +89,7 @@ hipError_t launch_expand_hist(int W, const uint64_t *rec, const Chunk *chunks, u
 hipError_t launch_cell_prefix(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, uint32_t *hist,
                               uint64_t *cell_total, hipStream_t s);
 hipError_t launch_expand_scatter(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
-                                 const uint32_t *hist, const uint64_t *cell_base, uint64_t *keys, hipStream_t s);
+                                 const uint32_t *hist, const uint64_t *cell_base, uint64_t *keys, int wc, hipStream_t s);
 hipError_t launch_bucket_flags(const uint64_t *cell_base, const uint64_t *cell_total, uint32_t nlbins, int F,
                                uint32_t small_cap, uint32_t group, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags, const uint64_t *flag_scan,
