@@ -181,6 +181,9 @@ struct fk_ctx {
     uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: cap/4)
     int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
+    int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
+    int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
+                               // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
 
     // input
     // host ingest: bytes are streamed to fasta_own (appended until the next fk_map)
@@ -204,7 +207,7 @@ struct fk_ctx {
     DevBuf precs, chunks, bin_chunk_begin;
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
-    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc;
+    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list;
     DevBuf table_off, tkeys, tstate, tcounts;
     ScanWorkspace ws;
     // results
@@ -334,6 +337,10 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->scatter_wc = (sc && sc[0]) ? atoi(sc) : 1;
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
+    const char *bp = getenv("FASTKMER_WAVE_BPW");
+    if (bp && bp[0]) c->wave_bpw = atoi(bp);
+    const char *cm = getenv("FASTKMER_COUNT_MODE");
+    if (cm && cm[0]) c->count_mode = atoi(cm);
     if (cfg->device >= 0) {
         if (cfg->device >= ndev) {
             delete c;
@@ -373,7 +380,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
-                      &c->tcounts};
+                      &c->tcounts, &c->tier_list};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -752,8 +759,16 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
                                   c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
                                   max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
-    HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
-                                cap - cap / 4, c->flags.as<uint32_t>(), s));
+    // 4c: buckets.  Tiered (k <= 32): cells packed greedily into buckets of
+    // <= WAVE_BUCKET_CAP keys for the wave kernel, larger cells to the block
+    // kernel (<= cap) or the large path.  Otherwise buckets of <= cap keys.
+    const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
+    if (tiered)
+        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, WAVE_BUCKET_CAP,
+                                           c->flags.as<uint32_t>(), s));
+    else
+        HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
+                                    cap - cap / 4, c->flags.as<uint32_t>(), s));
     HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), ncell_all,
                                      c->flag_scan.as<uint64_t>() + ncell_all, c->ws, s));
     uint64_t nbuckets = 0;
@@ -769,28 +784,54 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // 5: exact count per bucket in LDS; buckets that do not fit take the streaming path
     const uint32_t small_limit = c->force_large ? 0u : cap;
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
-    if (c->KW == 1)
-        HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
-                                      c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                      c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit,
-                                      c->dbg_phase, s));
-    else
-        HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
-                                   c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                   c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(), small_limit,
-                                   s));
-    uint64_t oversize = 0;
-    HIP_TRY(hipMemcpyAsync(&oversize, c->misc.p, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    c->stats.oversize_buckets = oversize;
     c->stats.buckets = nbuckets;
     c->stats.fine_bits = (uint64_t)F;
-    if (oversize) {
-        FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-        HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
-                                         c->scratch.as<uint64_t>(),
-                                         c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                         c->bucket_unique.as<uint64_t>(), s));
+    if (tiered) {
+        FK_TRY(ensure(c->tier_list, nbuckets * 8));
+        uint32_t *block_list = c->tier_list.as<uint32_t>(), *large_list = block_list + nbuckets;
+        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, cap, c->bucket_unique.as<uint64_t>(),
+                                    block_list, large_list, c->misc.as<unsigned int>(), s));
+        HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                           c->bucket_unique.as<uint64_t>(), c->wave_bpw, s));
+        uint32_t ntier[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (ntier[0])
+            HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[0], k,
+                                          c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                          c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
+                                          cap, 99, block_list, s));
+        if (ntier[1]) {
+            FK_TRY(ensure(c->scratch, total_kmers * 8));
+            HIP_TRY(launch_bucket_sort_large(1, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[1], k,
+                                             c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
+                                             c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
+                                             large_list, s));
+        }
+        c->stats.oversize_buckets = ntier[1];
+    } else {
+        if (c->KW == 1)
+            HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+                                          c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                          c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
+                                          small_limit, c->dbg_phase, nullptr, s));
+        else
+            HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+                                       c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                       c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
+                                       small_limit, s));
+        uint64_t oversize = 0;
+        HIP_TRY(hipMemcpyAsync(&oversize, c->misc.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->stats.oversize_buckets = oversize;
+        if (oversize) {
+            FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+            HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+                                             c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
+                                             c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
+                                             nullptr, s));
+        }
     }
     HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));

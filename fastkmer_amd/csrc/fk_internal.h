@@ -97,13 +97,22 @@ hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags,
                                hipStream_t s);
 hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                                 unsigned long long *oversize, uint32_t small_limit, int dbg_phase, hipStream_t s);
+                                 unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
+                                 const uint32_t *list, hipStream_t s);
+constexpr uint32_t WAVE_BUCKET_CAP = 512;  // keys per wave-tier bucket (k_bucket_count64_wave)
+hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
+                                      uint32_t *flags, hipStream_t s);
+hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t block_cap, uint64_t *bucket_unique,
+                               uint32_t *block_list, uint32_t *large_list, unsigned int *counts, hipStream_t s);
+hipError_t launch_bucket_count64_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
+                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique, int bpw,
+                                      hipStream_t s);
 hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, hipStream_t s);
 hipError_t launch_bucket_sort_large(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                                     uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
-                                    uint64_t *bucket_unique, hipStream_t s);
+                                    uint64_t *bucket_unique, const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_t *out_counts,
                                  const Bucket *buckets, uint64_t nbuckets, const uint64_t *dense_off,
                                  uint64_t *dense_keys, uint32_t *dense_counts, hipStream_t s);
