@@ -181,6 +181,7 @@ struct fk_ctx {
     uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: cap/4)
     int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
+    int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
                                // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
@@ -207,7 +208,7 @@ struct fk_ctx {
     DevBuf precs, chunks, bin_chunk_begin;
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
-    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list;
+    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_off;
     DevBuf table_off, tkeys, tstate, tcounts;
     ScanWorkspace ws;
     // results
@@ -337,6 +338,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->scatter_wc = (sc && sc[0]) ? atoi(sc) : 1;
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
+    const char *el = getenv("FASTKMER_EXPAND_LEVELS");
+    if (el && el[0]) c->expand_levels = atoi(el);
     const char *bp = getenv("FASTKMER_WAVE_BPW");
     if (bp && bp[0]) c->wave_bpw = atoi(bp);
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -380,7 +383,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
-                      &c->tcounts, &c->tier_list};
+                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_off};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -756,9 +759,19 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         for (int l = 0; l < 40; ++l)
             if (hc[l]) fprintf(stderr, "cells <2^%d: %llu cells %llu keys\n", l, (unsigned long long)hc[l], (unsigned long long)hk[l]);
     }
-    HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
-                                  c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
-                                  max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
+    if (c->W == 2 && c->expand_levels == 2) {
+        // two-level expansion: super-cells of the top F - F2 bits, then cells
+        const int F2 = std::min(F, 6);
+        FK_TRY(ensure(c->mid, total_kmers * 8));
+        FK_TRY(ensure(c->sc_off, ((uint64_t)nchunks << (F - F2)) * 8));
+        HIP_TRY(launch_expand_two_level(c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->nlb, k, F, F2,
+                                        c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->sc_off.as<uint64_t>(),
+                                        c->mid.as<uint64_t>(), c->keys.as<uint64_t>(), s));
+    } else {
+        HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+                                      c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
+                                      max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
+    }
     // 4c: buckets.  Tiered (k <= 32): cells packed greedily into buckets of
     // <= WAVE_BUCKET_CAP keys for the wave kernel, larger cells to the block
     // kernel (<= cap) or the large path.  Otherwise buckets of <= cap keys.

@@ -99,7 +99,10 @@ hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buck
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
                                  const uint32_t *list, hipStream_t s);
-constexpr uint32_t WAVE_BUCKET_CAP = 512;  // keys per wave-tier bucket (k_bucket_count64_wave)
+constexpr uint32_t WAVE_BUCKET_CAP = 512;
+hipError_t launch_expand_two_level(const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, uint32_t nlbins, int k,
+                                   int F, int F2, const uint32_t *lp, const uint64_t *cell_base, uint64_t *sc_off,
+                                   uint64_t *mid, uint64_t *keys, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
 hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
                                       uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t block_cap, uint64_t *bucket_unique,

@@ -273,6 +273,7 @@ hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWo
 #include "fk_partition.inc"
 #include "fk_radix_rank.inc"
 #include "fk_count_sorted.inc"
+#include "fk_expand2.inc"
 #include "fk_sort_radix.inc"
 #include "fk_compact.inc"
 #include "fk_count_hash.inc"

@@ -7,6 +7,7 @@ import fastkmer_amd as fk
 args = [a for a in sys.argv[1:] if "=" in a and not a.startswith("--")]
 reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
 nbytes = int(sys.argv[sys.argv.index("--bytes") + 1]) if "--bytes" in sys.argv else 1_000_000_000
+B = int(sys.argv[sys.argv.index("--B") + 1]) if "--B" in sys.argv else 2048
 axes = [(a.split("=")[0], a.split("=")[1].split(",")) for a in args]
 combos = list(itertools.product(*[[(n, v) for v in vals] for n, vals in axes]))
 best = {}
@@ -14,7 +15,7 @@ for rep in range(reps):
     for combo in combos:
         for n, v in combo:
             os.environ[n] = v
-        kc = fk.KmerCounter(28, 10, 3, 2048)
+        kc = fk.KmerCounter(28, 10, 3, B)
         kc.synth_device(nbytes // 114, 100, 100_000_000, seed=0x5EED)
         st = None
         for i in range(3):
@@ -28,5 +29,5 @@ for rep in range(reps):
         if prev is None or st["ms_count"] < prev["ms_count"]:
             best[key] = st
 for key, st in best.items():
-    print(f"{key}: count {st['ms_count']:.2f} ms  partition {st['ms_partition']:.2f}  sig {st['ms_signature']:.2f} "
+    print(f"B={B} {key}: count {st['ms_count']:.2f} ms  partition {st['ms_partition']:.2f}  sig {st['ms_signature']:.2f} "
           f"parse {st['ms_parse']:.2f}  distinct {st['distinct']}", flush=True)
