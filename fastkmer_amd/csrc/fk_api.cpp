@@ -182,6 +182,7 @@ struct fk_ctx {
     int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
     int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
+    uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
                                // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
@@ -340,6 +341,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
     const char *el = getenv("FASTKMER_EXPAND_LEVELS");
     if (el && el[0]) c->expand_levels = atoi(el);
+    const char *wc = getenv("FASTKMER_WAVE_CAP");
+    if (wc && wc[0]) c->wave_cap = (uint32_t)atoi(wc);
     const char *bp = getenv("FASTKMER_WAVE_BPW");
     if (bp && bp[0]) c->wave_bpw = atoi(bp);
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -777,7 +780,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // kernel (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, WAVE_BUCKET_CAP,
+        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, c->wave_cap,
                                            c->flags.as<uint32_t>(), s));
     else
         HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
@@ -802,11 +805,11 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     if (tiered) {
         FK_TRY(ensure(c->tier_list, nbuckets * 8));
         uint32_t *block_list = c->tier_list.as<uint32_t>(), *large_list = block_list + nbuckets;
-        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, cap, c->bucket_unique.as<uint64_t>(),
+        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, c->wave_cap, cap, c->bucket_unique.as<uint64_t>(),
                                     block_list, large_list, c->misc.as<unsigned int>(), s));
         HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
                                            c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                           c->bucket_unique.as<uint64_t>(), c->wave_bpw, s));
+                                           c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, s));
         uint32_t ntier[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
