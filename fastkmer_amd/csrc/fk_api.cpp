@@ -762,11 +762,15 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         for (int l = 0; l < 40; ++l)
             if (hc[l]) fprintf(stderr, "cells <2^%d: %llu cells %llu keys\n", l, (unsigned long long)hc[l], (unsigned long long)hk[l]);
     }
-    if (c->W == 2 && c->expand_levels == 2) {
-        // two-level expansion: super-cells of the top F - F2 bits, then cells
-        const int F2 = std::min(F, 6);
+    // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
+    const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
+    const bool two_level = c->W == 2 && c->expand_levels >= 2;
+    const int F2 = std::min(F, 6), F1 = F - F2;
+    if (two_level) {
         FK_TRY(ensure(c->mid, total_kmers * 8));
-        FK_TRY(ensure(c->sc_off, ((uint64_t)nchunks << (F - F2)) * 8));
+        FK_TRY(ensure(c->sc_off, ((uint64_t)nchunks << F1) * 8));
+    }
+    if (two_level) {
         HIP_TRY(launch_expand_two_level(c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->nlb, k, F, F2,
                                         c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->sc_off.as<uint64_t>(),
                                         c->mid.as<uint64_t>(), c->keys.as<uint64_t>(), s));
@@ -776,11 +780,10 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
                                       max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
     }
     // 4c: buckets.  Tiered (k <= 32): cells packed greedily into buckets of
-    // <= WAVE_BUCKET_CAP keys for the wave kernel, larger cells to the block
-    // kernel (<= cap) or the large path.  Otherwise buckets of <= cap keys.
-    const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
+    // <= wave_cap keys for the wave kernel, larger cells to the block kernel
+    // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, c->wave_cap,
+        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, c->wave_cap, -1,
                                            c->flags.as<uint32_t>(), s));
     else
         HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
@@ -804,12 +807,13 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     c->stats.fine_bits = (uint64_t)F;
     if (tiered) {
         FK_TRY(ensure(c->tier_list, nbuckets * 8));
-        uint32_t *block_list = c->tier_list.as<uint32_t>(), *large_list = block_list + nbuckets;
-        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, c->wave_cap, cap, c->bucket_unique.as<uint64_t>(),
-                                    block_list, large_list, c->misc.as<unsigned int>(), s));
+        uint32_t *lists = c->tier_list.as<uint32_t>();
+        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, c->wave_cap, cap,
+                                    c->bucket_unique.as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
+        // every bucket of <= wave_cap keys
         HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
                                            c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                           c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, s));
+                                           c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, nullptr, s));
         uint32_t ntier[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -817,13 +821,13 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
             HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[0], k,
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
-                                          cap, 99, block_list, s));
+                                          cap, 99, lists, s));
         if (ntier[1]) {
             FK_TRY(ensure(c->scratch, total_kmers * 8));
             HIP_TRY(launch_bucket_sort_large(1, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
-                                             large_list, s));
+                                             lists + nbuckets, s));
         }
         c->stats.oversize_buckets = ntier[1];
     } else {

@@ -104,13 +104,12 @@ hipError_t launch_expand_two_level(const uint64_t *rec, const Chunk *chunks, uin
                                    int F, int F2, const uint32_t *lp, const uint64_t *cell_base, uint64_t *sc_off,
                                    uint64_t *mid, uint64_t *keys, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
 hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
-                                      uint32_t *flags, hipStream_t s);
+                                      int period_bits, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
-                               uint64_t *bucket_unique, uint32_t *block_list, uint32_t *large_list, unsigned int *counts,
-                               hipStream_t s);
+                               uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts, hipStream_t s);
 hipError_t launch_bucket_count64_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique, int bpw,
-                                      uint32_t wave_cap, hipStream_t s);
+                                      uint32_t wave_cap, const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, hipStream_t s);
