@@ -380,3 +380,36 @@ def test_full_size_properties():
     assert st["distinct"] == int(sizes.sum())
     assert all_counts == st["kmers"]
     assert st["kmers"] > 0.9 * n_reads * 73
+
+
+def test_big_bins_two_level_vs_oracle():
+    # few, large bins (~800K k-mers each): 2^11 cells per bin, 32 super-cells
+    # (the two-level expansion with F1 > 0) and all three count tiers
+    fasta = fk.synth_fasta(350_000, 100, 3_000_000, seed=53)
+    kc = run_counter(fasta, 28, 10, 3, 32)
+    st = kc.stats()
+    assert st["fine_bits"] >= 9
+    ref = oracle.OracleResult(fasta, 28, 10, 32)
+    assert st["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref)
+
+
+@pytest.mark.parametrize("env", [
+    {"FASTKMER_COUNT_MODE": "0"},                                   # one workgroup per <= 2048-key bucket
+    {"FASTKMER_EXPAND_LEVELS": "1"},                                # one-level write-combined scatter
+    {"FASTKMER_EXPAND_LEVELS": "1", "FASTKMER_DEBUG_SCATTER": "0"},  # plain scatter
+    {"FASTKMER_WAVE_CAP": "256", "FASTKMER_WAVE_BPW": "1"},
+    {"FASTKMER_WAVE_CAP": "128", "FASTKMER_WAVE_BPW": "2", "FASTKMER_DEBUG_CELL_TARGET": "64"},
+])
+def test_count_variants_identical(monkeypatch, env):
+    # every count-stage variant gives the default path's result, bit for bit
+    fasta = fk.synth_fasta(120_000, 100, 1_000_000, seed=59)
+    base = run_counter(fasta, 27, 9, 3, 128)
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    alt = run_counter(fasta, 27, 9, 3, 128)
+    assert np.array_equal(base.bin_sizes(), alt.bin_sizes())
+    for b in range(0, 128, 7):
+        kb, cb = base.get_bin(b)
+        ka, ca = alt.get_bin(b)
+        assert np.array_equal(kb, ka) and np.array_equal(cb, ca)
