@@ -209,7 +209,7 @@ struct fk_ctx {
     DevBuf precs, chunks, bin_chunk_begin;
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
-    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_off;
+    DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_total;
     DevBuf table_off, tkeys, tstate, tcounts;
     ScanWorkspace ws;
     // results
@@ -386,7 +386,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
-                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_off};
+                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_total};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -729,13 +729,18 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // cell bits: the largest bin's cells average cap/4 keys (a bucket groups a
     // few cells; runs of one chunk's keys per cell stay long enough to be
     // written as whole lines)
-    const uint64_t target = c->cell_target ? c->cell_target : cap / 4;
+    // (two-level expansion: cap / 8, measured faster; the wave tier then holds
+    // nearly every cell)
+    const uint64_t target = c->cell_target ? c->cell_target : (c->W == 2 && c->expand_levels >= 2 ? cap / 8 : cap / 4);
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
-    FK_TRY(ensure(c->lp, (uint64_t)nchunks * ncell * 4));
+    // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
+    const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
+    const bool two_level = c->W == 2 && c->expand_levels >= 2;
+    const int F2 = std::min(F, 6), F1 = F - F2;
     FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
@@ -743,10 +748,23 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
     // 4: expand records -> canonical k-mers, laid out bin-major by cell
-    HIP_TRY(launch_expand_hist(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
-                               c->lp.as<uint32_t>(), s));
-    HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
-                               c->cell_total.as<uint64_t>(), s));
+    if (two_level) {
+        // cell totals by atomics, per-chunk counts only per super-cell
+        const uint64_t nsc_all = (uint64_t)c->nlb << F1;
+        FK_TRY(ensure(c->lp, ((uint64_t)nchunks << F1) * 4));
+        FK_TRY(ensure(c->sc_total, nsc_all * 8));
+        HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
+        HIP_TRY(launch_expand_hist_sc(c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F, F2,
+                                      c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
+        HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F1, c->lp.as<uint32_t>(),
+                                   c->sc_total.as<uint64_t>(), s));
+    } else {
+        FK_TRY(ensure(c->lp, (uint64_t)nchunks * ncell * 4));
+        HIP_TRY(launch_expand_hist(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+                                   c->lp.as<uint32_t>(), s));
+        HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
+                                   c->cell_total.as<uint64_t>(), s));
+    }
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
                               c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
     if (getenv("FASTKMER_DEBUG_CELL_SIZES")) {  // key-weighted histogram of log2(cell size), stderr
@@ -762,18 +780,11 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         for (int l = 0; l < 40; ++l)
             if (hc[l]) fprintf(stderr, "cells <2^%d: %llu cells %llu keys\n", l, (unsigned long long)hc[l], (unsigned long long)hk[l]);
     }
-    // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
-    const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
-    const bool two_level = c->W == 2 && c->expand_levels >= 2;
-    const int F2 = std::min(F, 6), F1 = F - F2;
     if (two_level) {
         FK_TRY(ensure(c->mid, total_kmers * 8));
-        FK_TRY(ensure(c->sc_off, ((uint64_t)nchunks << F1) * 8));
-    }
-    if (two_level) {
         HIP_TRY(launch_expand_two_level(c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->nlb, k, F, F2,
-                                        c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->sc_off.as<uint64_t>(),
-                                        c->mid.as<uint64_t>(), c->keys.as<uint64_t>(), s));
+                                        c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->mid.as<uint64_t>(),
+                                        c->keys.as<uint64_t>(), s));
     } else {
         HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
                                       c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),

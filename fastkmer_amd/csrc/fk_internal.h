@@ -22,7 +22,7 @@ constexpr int SIG_TILE = 4096;   // k-mer start positions per signature workgrou
 constexpr int SIG_PPT = 16;      // positions per thread == max k-mers per record
 constexpr int POS_PAD_WORDS = 64;  // zero words after the packed stream (halo reads)
 constexpr int SORT_CAP = 4096;   // keys per LDS-sorted bucket (u64 keys; half for 128-bit keys)
-constexpr int MAX_FINE_BITS = 13;
+constexpr int MAX_FINE_BITS = 15;
 
 // record header (low 32 bits of word 0): bin | (n-1) << 22
 constexpr int REC_BIN_BITS = 22;
@@ -101,8 +101,10 @@ hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buck
                                  const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
 hipError_t launch_expand_two_level(const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, uint32_t nlbins, int k,
-                                   int F, int F2, const uint32_t *lp, const uint64_t *cell_base, uint64_t *sc_off,
-                                   uint64_t *mid, uint64_t *keys, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
+                                   int F, int F2, const uint32_t *sc_pre, const uint64_t *cell_base, uint64_t *mid,
+                                   uint64_t *keys, hipStream_t s);
+hipError_t launch_expand_hist_sc(const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F, int F2,
+                                 uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
 hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
                                       int period_bits, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
