@@ -57,6 +57,30 @@ def cpu_baseline(sample_bytes: int) -> dict:
                       f"oracle/fk_oracle.c single-threaded, {dt:.1f} s, {r.total_kmers} k-mers"}
 
 
+def long_sequence_fasta(n_bases: int, seed: int = 0x5EED) -> bytes:
+    """BASELINE configs[4] shape: one '>chrSynthetic' record,
+    60-column lines, uniform ACGT with 100 runs of 10 kbp of N and 5% of
+    the bases soft-masked (lowercase, invalid for the reference)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    seq = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, n_bases, dtype=np.uint8)].copy()
+    for start in rng.integers(0, max(1, n_bases - 10_000), 100):
+        seq[start:start + 10_000] = ord("N")
+    for start in rng.integers(0, max(1, n_bases - 50_000), max(1, n_bases // 1_000_000)):
+        seq[start:start + 50_000] |= 0x20  # lowercase
+    n_lines = (n_bases + 59) // 60
+    body = np.full(n_lines * 61, ord("\n"), dtype=np.uint8)
+    view = body.reshape(n_lines, 61)
+    full = np.zeros(n_lines * 60, dtype=np.uint8)
+    full[:n_bases] = seq
+    view[:, :60] = full.reshape(n_lines, 60)
+    out = body.tobytes()
+    tail = n_lines * 60 - n_bases  # drop the padding of the last line
+    if tail:
+        out = out[:len(out) - 1 - tail] + b"\n"
+    return b">chrSynthetic\n" + out
+
+
 def load_traffic():
     """HBM bytes per launch of the encode+signature stage from the committed
     rocprofv3 PMC summary (profiles/), if present."""
@@ -81,6 +105,10 @@ def main() -> None:
                          "ingests it (H2D) before counting; reported as a separate metric, never as the headline")
     ap.add_argument("--balance", action="store_true",
                     help="size-aware bin placement (reference useCustomPartitioner=1) instead of bin %% N")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
+                    help="c2 = BASELINE configs[1] (the metric's workload, default); c4 = configs[3] shape "
+                         "(k=55 m=12 B=8192, 150 bp reads, two-word keys); c5 = configs[4] shape "
+                         "(sequenceType=1, one long record, host-generated, ingested before timing)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo stages records through host memory "
                          "(rehearsal of N > 1 with ranks sharing a GPU)")
@@ -99,14 +127,28 @@ def main() -> None:
         else:
             dist.init_process_group("gloo")
 
-    n_reads = args.bytes_per_gpu // REC_BYTES
-    kc = fk.KmerCounter(K, M, X, B, use_ht=False, sequence_type=0, n_ranks=world, rank=rank,
+    k, m, x, b, read_len, seq_type = K, M, X, B, READ_LEN, 0
+    if args.workload == "c4":
+        k, m, b, read_len = 55, 12, 8192, 150
+    elif args.workload == "c5":
+        seq_type = 1
+    rec_bytes = read_len + 14
+    n_reads = args.bytes_per_gpu // rec_bytes
+    kc = fk.KmerCounter(k, m, x, b, use_ht=False, sequence_type=seq_type, n_ranks=world, rank=rank,
                         device=gpu)
-    # per-rank shard of one synthetic read set (weak scaling: 1 GB per GPU)
-    fasta_bytes = kc.synth_device(n_reads, READ_LEN, GENOME, seed=SEED, first_read=rank * n_reads)
-    bases_per_rank = n_reads * READ_LEN
+    if args.workload == "c5":
+        # one long record per rank (weak scaling), resident on the device before timing
+        n_bases = args.bytes_per_gpu * 60 // 61
+        data = long_sequence_fasta(n_bases, seed=SEED + rank)
+        kc.ingest(data)
+        fasta_bytes, bases_per_rank = len(data), n_bases
+        del data
+    else:
+        # per-rank shard of one synthetic read set (weak scaling: 1 GB per GPU)
+        fasta_bytes = kc.synth_device(n_reads, read_len, GENOME, seed=SEED, first_read=rank * n_reads)
+        bases_per_rank = n_reads * read_len
     host_buf = None
-    if args.host_input:  # the same shard in pinned host memory, prepared outside the timed region
+    if args.host_input and args.workload == "c2":  # the same shard in pinned host memory, prepared outside the timed region
         import numpy as np
         host_buf = torch.empty(fasta_bytes, dtype=torch.uint8).pin_memory()
         host_buf.copy_(torch.from_numpy(np.frombuffer(
@@ -155,6 +197,12 @@ def main() -> None:
         t_es = sum(stage_ms) / len(stage_ms) * 1e-3
         achieved = fasta_bytes / t_es
         metric = "input bases/sec (whole node), k=28 short reads, 1/2/4/8 GPUs; counts bit-exact"
+        workload = {"c2": "BASELINE configs[1]: k=28 m=10 x=3 B=2048, 1 GB synthetic 100 bp reads per GPU",
+                    "c4": "BASELINE configs[3] shape: k=55 m=12 x=3 B=8192, 1 GB synthetic 150 bp reads per GPU",
+                    "c5": "BASELINE configs[4] shape: sequenceType=1, one synthetic long record "
+                          "(60-col lines, 100 x 10 kbp N runs, 5% soft-masked) of 1 GB per GPU"}[args.workload]
+        if args.workload != "c2":
+            metric += f" [{args.workload} workload, not the headline configuration]"
         if args.host_input:
             metric += " [PCIe-inclusive variant: FASTA in pinned host memory, H2D inside every step]"
         out = {
@@ -169,9 +217,11 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (device-generated 100 bp reads, 100 Mbp virtual genome, 0.2% subst, 0.05% N)",
-            "config": {"workload": "BASELINE configs[1]: k=28 m=10 x=3 B=2048, 1 GB synthetic 100 bp reads per GPU",
-                       "k": K, "m": M, "x": X, "B": B, "useHT": 0, "fasta_bytes_per_gpu": fasta_bytes,
+            "data": ("synthetic (device-generated %d bp reads, 100 Mbp virtual genome, 0.2%% subst, 0.05%% N)" % read_len
+                     if args.workload != "c5" else "synthetic long record (host-generated, ingested before timing)"),
+            "config": {"workload": workload,
+                       "k": k, "m": m, "x": x, "B": b, "useHT": 0, "sequenceType": seq_type,
+                       "fasta_bytes_per_gpu": fasta_bytes,
                        "bases_per_gpu": bases_per_rank, "parallelism": (f"bins placed by size (LPT) over {world} GPU(s)" if args.balance and distributed
                                            else f"bins round-robin over {world} GPU(s)")},
             "roofline": {"bound": "hbm",
@@ -184,7 +234,7 @@ def main() -> None:
                           "partition": stats["ms_partition"], "count": stats["ms_count"]},
             "kmers_per_gpu": stats["kmers"], "distinct_rank0": stats["distinct"],
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "c2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_bytes)
         print(json.dumps(out), flush=True)
     kc.close()

@@ -731,15 +731,15 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // written as whole lines)
     // (two-level expansion: cap / 8, measured faster; the wave tier then holds
     // nearly every cell)
-    const uint64_t target = c->cell_target ? c->cell_target : (c->W == 2 && c->expand_levels >= 2 ? cap / 8 : cap / 4);
+    const bool tiered = (c->KW == 1 || c->cfg.k <= 63) && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
+    const bool two_level = c->W == 2 && c->expand_levels >= 2;
+    const uint64_t target = c->cell_target ? c->cell_target : (two_level || tiered ? cap / 8 : cap / 4);
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
-    const bool tiered = c->KW == 1 && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
-    const bool two_level = c->W == 2 && c->expand_levels >= 2;
     const int F2 = std::min(F, 6), F1 = F - F2;
     FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
@@ -822,20 +822,30 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, c->wave_cap, cap,
                                     c->bucket_unique.as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
         // every bucket of <= wave_cap keys
-        HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
-                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                           c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, nullptr, s));
+        if (c->KW == 1)
+            HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+                                               c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                               c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, nullptr, s));
+        else
+            HIP_TRY(launch_bucket_count128_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+                                                c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                                c->bucket_unique.as<uint64_t>(), s));
         uint32_t ntier[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (ntier[0])
+        if (ntier[0] && c->KW == 1)
             HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[0], k,
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
                                           cap, 99, lists, s));
+        else if (ntier[0])
+            HIP_TRY(launch_bucket_sort(2, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[0], k,
+                                       c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                       c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
+                                       lists, s));
         if (ntier[1]) {
-            FK_TRY(ensure(c->scratch, total_kmers * 8));
-            HIP_TRY(launch_bucket_sort_large(1, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[1], k,
+            FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+            HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              lists + nbuckets, s));
@@ -851,7 +861,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
             HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
-                                       small_limit, s));
+                                       small_limit, nullptr, s));
         uint64_t oversize = 0;
         HIP_TRY(hipMemcpyAsync(&oversize, c->misc.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

@@ -100,6 +100,9 @@ hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buck
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
                                  const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
+hipError_t launch_bucket_count128_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
+                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+                                       hipStream_t s);
 hipError_t launch_expand_two_level(const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, uint32_t nlbins, int k,
                                    int F, int F2, const uint32_t *sc_pre, const uint64_t *cell_base, uint64_t *mid,
                                    uint64_t *keys, hipStream_t s);
@@ -114,7 +117,7 @@ hipError_t launch_bucket_count64_wave(const uint64_t *keys, int F, const Bucket 
                                       uint32_t wave_cap, const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                              unsigned long long *oversize, uint32_t small_limit, hipStream_t s);
+                              unsigned long long *oversize, uint32_t small_limit, const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_sort_large(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                                     uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
                                     uint64_t *bucket_unique, const uint32_t *list, hipStream_t s);
