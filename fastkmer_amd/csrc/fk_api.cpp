@@ -183,6 +183,7 @@ struct fk_ctx {
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
     int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
+    int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
                                // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
@@ -343,6 +344,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (el && el[0]) c->expand_levels = atoi(el);
     const char *wc = getenv("FASTKMER_WAVE_CAP");
     if (wc && wc[0]) c->wave_cap = (uint32_t)atoi(wc);
+    const char *f2 = getenv("FASTKMER_F2");
+    if (f2 && f2[0]) c->f2_bits = std::max(0, std::min(9, atoi(f2)));
     const char *bp = getenv("FASTKMER_WAVE_BPW");
     if (bp && bp[0]) c->wave_bpw = atoi(bp);
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -740,7 +743,8 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
-    const int F2 = std::min(F, 6), F1 = F - F2;
+    // cells per super-cell: 2^5 up to F = 13, 2^6 above (measured at configs[1] and at 8x larger bins)
+    const int F2 = std::min(F, c->f2_bits >= 0 ? c->f2_bits : std::max(5, std::min(6, F - 8))), F1 = F - F2;
     FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
