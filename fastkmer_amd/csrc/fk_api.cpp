@@ -736,7 +736,8 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // nearly every cell)
     const bool tiered = (c->KW == 1 || c->cfg.k <= 63) && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
     const bool two_level = c->W == 2 && c->expand_levels >= 2;
-    const uint64_t target = c->cell_target ? c->cell_target : (two_level || tiered ? cap / 8 : cap / 4);
+    const uint64_t target = c->cell_target ? c->cell_target
+                                           : (two_level ? cap / 8 : tiered ? WAVE128_BUCKET_CAP / 2 : cap / 4);
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
@@ -744,6 +745,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
     // cells per super-cell: 2^5 up to F = 13, 2^6 above (measured at configs[1] and at 8x larger bins)
+    const uint32_t wave_cap = c->KW == 1 ? c->wave_cap : WAVE128_BUCKET_CAP;
     const int F2 = std::min(F, c->f2_bits >= 0 ? c->f2_bits : std::max(5, std::min(6, F - 8))), F1 = F - F2;
     FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
@@ -798,7 +800,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, c->wave_cap, -1,
+        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, wave_cap, -1,
                                            c->flags.as<uint32_t>(), s));
     else
         HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
@@ -823,7 +825,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     if (tiered) {
         FK_TRY(ensure(c->tier_list, nbuckets * 8));
         uint32_t *lists = c->tier_list.as<uint32_t>();
-        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, c->wave_cap, cap,
+        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, wave_cap, cap,
                                     c->bucket_unique.as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
