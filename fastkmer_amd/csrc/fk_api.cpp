@@ -735,9 +735,9 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // (two-level expansion: cap / 8, measured faster; the wave tier then holds
     // nearly every cell)
     const bool tiered = (c->KW == 1 || c->cfg.k <= 63) && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
-    const bool two_level = c->W == 2 && c->expand_levels >= 2;
+    const bool two_level = (c->W == 2 || c->cfg.k <= 63) && c->expand_levels >= 2;
     const uint64_t target = c->cell_target ? c->cell_target
-                                           : (two_level ? cap / 8 : tiered ? WAVE128_BUCKET_CAP / 2 : cap / 4);
+                                           : (c->KW == 2 && tiered ? WAVE128_BUCKET_CAP / 2 : two_level ? cap / 8 : cap / 4);
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     F = std::min(F, 2 * k);
@@ -760,7 +760,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         FK_TRY(ensure(c->lp, ((uint64_t)nchunks << F1) * 4));
         FK_TRY(ensure(c->sc_total, nsc_all * 8));
         HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
-        HIP_TRY(launch_expand_hist_sc(c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F, F2,
+        HIP_TRY(launch_expand_hist_sc(c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F, F2,
                                       c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
         HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F1, c->lp.as<uint32_t>(),
                                    c->sc_total.as<uint64_t>(), s));
@@ -787,9 +787,9 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
             if (hc[l]) fprintf(stderr, "cells <2^%d: %llu cells %llu keys\n", l, (unsigned long long)hc[l], (unsigned long long)hk[l]);
     }
     if (two_level) {
-        FK_TRY(ensure(c->mid, total_kmers * 8));
-        HIP_TRY(launch_expand_two_level(c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->nlb, k, F, F2,
-                                        c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->mid.as<uint64_t>(),
+        FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
+        HIP_TRY(launch_expand_two_level(c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
+                                        F2, c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->mid.as<uint64_t>(),
                                         c->keys.as<uint64_t>(), s));
     } else {
         HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,

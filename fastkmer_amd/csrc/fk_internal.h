@@ -104,11 +104,11 @@ constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-
 hipError_t launch_bucket_count128_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                        hipStream_t s);
-hipError_t launch_expand_two_level(const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, uint32_t nlbins, int k,
-                                   int F, int F2, const uint32_t *sc_pre, const uint64_t *cell_base, uint64_t *mid,
-                                   uint64_t *keys, hipStream_t s);
-hipError_t launch_expand_hist_sc(const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F, int F2,
-                                 uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
+hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
+                                   uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
+                                   const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s);
+hipError_t launch_expand_hist_sc(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
+                                 int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
 hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
                                       int period_bits, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
