@@ -84,14 +84,16 @@ struct LbSum {
 // 0..tile-1 and publishes the inclusive value.  Values stay below 2^62.
 // Tiles are dispatched in blockIdx order, so every predecessor is resident
 // or finished and the spin terminates.
+// The two halves can be split (lookback_publish early, lookback_resolve once
+// the prefix is needed) so the wait overlaps the tile's own work.
+__device__ __forceinline__ void lookback_publish(uint64_t *status, uint64_t tile, uint64_t agg) {
+    if ((threadIdx.x & 63) == 0) lb_store(&status[tile], (tile == 0 ? LB_INC : LB_AGG) | agg);
+}
+
 template <class Op>
-__device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg, Op op) {
+__device__ uint64_t lookback_resolve(uint64_t *status, uint64_t tile, uint64_t agg, Op op) {
     const int lane = threadIdx.x & 63;
-    if (tile == 0) {
-        if (lane == 0) lb_store(&status[0], LB_INC | agg);
-        return Op::ident;
-    }
-    if (lane == 0) lb_store(&status[tile], LB_AGG | agg);
+    if (tile == 0) return Op::ident;
     uint64_t excl = Op::ident;
     int64_t pos = (int64_t)tile - 1;
     while (true) {
@@ -115,6 +117,12 @@ __device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg,
     }
     if (lane == 0) lb_store(&status[tile], LB_INC | op(excl, agg));
     return excl;
+}
+
+template <class Op>
+__device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg, Op op) {
+    lookback_publish(status, tile, agg);
+    return lookback_resolve(status, tile, agg, op);
 }
 
 // exclusive block prefix max (identity `ident`)
