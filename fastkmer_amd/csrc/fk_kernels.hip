@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <limits>
+
 #include "fk_internal.h"
 
 namespace fk {
@@ -21,26 +23,44 @@ constexpr int NT = 256;  // threads per workgroup (4 waves)
 // block-level helpers (256 threads)
 // ---------------------------------------------------------------------------
 
-template <typename T>
-__device__ __forceinline__ T wave_incl_sum(T v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T u = __shfl_up(v, d, 64);
-        if (lane >= d) v += u;
+// Wave-wide inclusive scans on DPP lane moves (row_shr within 16-lane rows,
+// then row_bcast:15 / row_bcast:31 across rows): no LDS round trips.
+// Lanes without a source keep `old` (the identity).
+template <int CTRL, int ROWM>
+__device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWM, 0xf, false);
+}
+template <int CTRL, int ROWM, typename T>
+__device__ __forceinline__ T dpp_move(T ident, T v) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit scan values");
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, dpp32<CTRL, ROWM>(__builtin_bit_cast(uint32_t, ident), __builtin_bit_cast(uint32_t, v)));
+    } else {
+        const uint64_t i = __builtin_bit_cast(uint64_t, ident), x = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = dpp32<CTRL, ROWM>((uint32_t)i, (uint32_t)x);
+        const uint32_t hi = dpp32<CTRL, ROWM>((uint32_t)(i >> 32), (uint32_t)(x >> 32));
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
     }
+}
+template <typename T, class F>
+__device__ __forceinline__ T wave_incl_scan(T v, T ident, F op) {
+    v = op(v, dpp_move<0x111, 0xf>(ident, v));  // row_shr:1
+    v = op(v, dpp_move<0x112, 0xf>(ident, v));  // row_shr:2
+    v = op(v, dpp_move<0x114, 0xf>(ident, v));  // row_shr:4
+    v = op(v, dpp_move<0x118, 0xf>(ident, v));  // row_shr:8
+    v = op(v, dpp_move<0x142, 0xa>(ident, v));  // row_bcast:15 -> rows 1, 3
+    v = op(v, dpp_move<0x143, 0xc>(ident, v));  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
 template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T v) {
+    return wave_incl_scan<T>(v, (T)0, [](T a, T b) { return a + b; });
+}
+
+template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T u = __shfl_up(v, d, 64);
-        if (lane >= d) v = u > v ? u : v;
-    }
-    return v;
+    return wave_incl_scan<T>(v, std::numeric_limits<T>::lowest(), [](T a, T b) { return a > b ? a : b; });
 }
 
 // exclusive block prefix sum; *total receives the block sum (all threads)
