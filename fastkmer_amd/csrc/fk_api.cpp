@@ -185,6 +185,7 @@ struct fk_ctx {
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
+    bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
     int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
                                // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
 
@@ -348,6 +349,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (f2 && f2[0]) c->f2_bits = std::max(0, std::min(9, atoi(f2)));
     const char *bp = getenv("FASTKMER_WAVE_BPW");
     if (bp && bp[0]) c->wave_bpw = atoi(bp);
+    const char *pl = getenv("FASTKMER_PARSE_LOOKBACK");
+    if (pl && pl[0]) c->parse_scan = atoi(pl) == 0;
     const char *cm = getenv("FASTKMER_COUNT_MODE");
     if (cm && cm[0]) c->count_mode = atoi(cm);
     if (cfg->device >= 0) {
@@ -549,7 +552,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     const uint64_t valid_words = n / 32 + 2 * POS_PAD_WORDS + 512;
     FK_TRY(ensure(c->tile_last_nl, ntiles * 8));  // look-back status: newline / header state
     FK_TRY(ensure(c->tile_off, ntiles * 8));      // look-back status: output positions
-    FK_TRY(ensure(c->npos_dev, 8));
+    FK_TRY(ensure(c->npos_dev, 16));  // [0] positions, [1] "rerun the parse with the look-back"
     FK_TRY(ensure(c->codes, code_words * 4));
     FK_TRY(ensure(c->valid, valid_words * 4));
     FK_TRY(ensure(c->counters, 64));
@@ -557,20 +560,29 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     FK_TRY(ensure(c->sig_status, sig_tiles * 8));
     FK_TRY(ensure(c->sig_kmers, sig_tiles * 8));
 
-    // 1. FASTA parse + 2-bit encode
-    HIP_TRY(hipEventRecord(c->ev[0], s));
-    HIP_TRY(hipMemsetAsync(c->codes.p, 0, code_words * 4, s));
-    HIP_TRY(hipMemsetAsync(c->valid.p, 0, valid_words * 4, s));
-    HIP_TRY(hipMemsetAsync(c->npos_dev.p, 0, 8, s));
-    if (n) {
-        HIP_TRY(hipMemsetAsync(c->tile_last_nl.p, 0, ntiles * 8, s));
-        HIP_TRY(hipMemsetAsync(c->tile_off.p, 0, ntiles * 8, s));
-        HIP_TRY(hipEventRecord(c->ev[8], s));
-        HIP_TRY(launch_fasta_parse(c->d_fasta, n, c->tile_last_nl.as<uint64_t>(), c->tile_off.as<uint64_t>(),
-                                   c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), c->npos_dev.as<uint64_t>(), s));
-        HIP_TRY(hipEventRecord(c->ev[9], s));
-    }
-    HIP_TRY(hipEventRecord(c->ev[1], s));
+    // 1. FASTA parse + 2-bit encode.  The scan variant flags inputs it cannot
+    // place (a line longer than its read-back, text before the first header);
+    // the flag is read with the record count below and the parse is redone
+    // with the line look-back.
+    auto run_parse = [&](bool scan) -> int {
+        HIP_TRY(hipEventRecord(c->ev[0], s));
+        HIP_TRY(hipMemsetAsync(c->codes.p, 0, code_words * 4, s));
+        HIP_TRY(hipMemsetAsync(c->valid.p, 0, valid_words * 4, s));
+        HIP_TRY(hipMemsetAsync(c->npos_dev.p, 0, 16, s));
+        if (n) {
+            if (!scan) HIP_TRY(hipMemsetAsync(c->tile_last_nl.p, 0, ntiles * 8, s));
+            HIP_TRY(hipMemsetAsync(c->tile_off.p, 0, ntiles * 8, s));
+            HIP_TRY(hipEventRecord(c->ev[8], s));
+            HIP_TRY(launch_fasta_parse(scan, c->d_fasta, n, c->tile_last_nl.as<uint64_t>(), c->tile_off.as<uint64_t>(),
+                                       c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), c->npos_dev.as<uint64_t>(),
+                                       s));
+            HIP_TRY(hipEventRecord(c->ev[9], s));
+        }
+        HIP_TRY(hipEventRecord(c->ev[1], s));
+        return FK_OK;
+    };
+    bool parse_scan = c->parse_scan;
+    FK_TRY(run_parse(parse_scan));
 
     // 2. signature + super-k-mer records (retried once if the capacity estimate was short)
     uint64_t rec_cap = std::max<uint64_t>(n / 6, 4096);
@@ -591,9 +603,16 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         HIP_TRY(scan_excl_sum_u64(c->sig_kmers.as<uint64_t>(), c->sig_status.as<uint64_t>(), sig_tiles,
                                   c->counters.as<uint64_t>() + 1, c->ws, s));
         HIP_TRY(hipEventRecord(c->ev[3], s));
-        uint64_t h[2];
+        uint64_t h[2], redo = 0;
         HIP_TRY(hipMemcpyAsync(h, c->counters.p, 16, hipMemcpyDeviceToHost, s));
+        if (parse_scan) HIP_TRY(hipMemcpyAsync(&redo, c->npos_dev.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (redo) {
+            parse_scan = false;
+            FK_TRY(run_parse(false));
+            --attempt;
+            continue;
+        }
         c->nrec = h[0];
         c->nkmers = h[1];
         if (c->nrec <= rec_cap) break;

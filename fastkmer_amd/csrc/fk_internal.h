@@ -54,8 +54,8 @@ hipError_t scan_excl_sum_u32_to_u64(const uint32_t *in, uint64_t *out, uint64_t 
 hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWorkspace &ws, hipStream_t s);
 
 // ---- FASTA parse + encode (records -> compacted packed positions)
-hipError_t launch_fasta_parse(const uint8_t *fa, uint64_t n, uint64_t *st_line, uint64_t *st_pos, uint32_t *codes,
-                              uint32_t *valid, uint64_t *npos_dev, hipStream_t s);
+hipError_t launch_fasta_parse(bool scan, const uint8_t *fa, uint64_t n, uint64_t *st_line, uint64_t *st_pos,
+                              uint32_t *codes, uint32_t *valid, uint64_t *npos_dev, hipStream_t s);
 hipError_t launch_superkmers(int W, const uint32_t *codes, const uint32_t *valid, uint64_t npos_bound,
                              const uint64_t *npos_dev, int k, int m, FastMod fm, uint64_t *records, uint64_t rec_cap,
                              uint64_t *status, uint64_t *tile_kmers, unsigned long long *counters, hipStream_t s);

@@ -413,3 +413,26 @@ def test_count_variants_identical(monkeypatch, env):
         kb, cb = base.get_bin(b)
         ka, ca = alt.get_bin(b)
         assert np.array_equal(kb, ka) and np.array_equal(cb, ca)
+
+
+@pytest.mark.parametrize("case", ["long_lines", "text_before_header", "forced_lookback"])
+def test_parse_line_lookback_paths_vs_oracle(monkeypatch, case):
+    # the parse finds the line holding each tile start by reading back 4 KB;
+    # lines longer than that (sequence or header) and text before the first
+    # header take the look-back rerun, which must give the same result
+    rng = random.Random(77)
+    if case == "long_lines":
+        big = "".join(rng.choice("ACGT") for _ in range(40_000))
+        hdr = "".join(rng.choice("ACGT>x ") for _ in range(30_000))
+        fasta = (random_fasta(rng, 200, 50, 150) + f">big\n{big}\n>{hdr}\nACGTTGCAACGTGGCCA\n".encode()
+                 + random_fasta(rng, 200, 50, 150))
+    elif case == "text_before_header":
+        fasta = b"ACGTACGTTTGACCAGGGTACCA\nGGGTTTACCAGT\n" + random_fasta(rng, 500, 50, 300)
+    else:
+        monkeypatch.setenv("FASTKMER_PARSE_LOOKBACK", "1")
+        fasta = random_fasta(rng, 2000, 50, 300, wrap=61)
+    for k, m in ((28, 10), (55, 12)):
+        kc = run_counter(fasta, k, m, 3, 512)
+        ref = oracle.OracleResult(fasta, k, m, 512)
+        assert kc.stats()["kmers"] == ref.total_kmers
+        assert_same_as_oracle(kc, ref)
