@@ -42,6 +42,8 @@ def lib():
         L.fko_count.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32,
                                 ctypes.c_int32, ctypes.c_int32]
         L.fko_count.restype = ctypes.c_void_p
+        L.fko_count_mt.argtypes = L.fko_count.argtypes + [ctypes.c_int32]
+        L.fko_count_mt.restype = ctypes.c_void_p
         for name in ("fko_total_kmers", "fko_superkmers", "fko_reads", "fko_distinct"):
             getattr(L, name).argtypes = [ctypes.c_void_p]
             getattr(L, name).restype = ctypes.c_int64
@@ -92,11 +94,14 @@ def kmer_to_string(hi: int, lo: int, k: int) -> str:
 class OracleResult:
     """Per-bin sorted (canonical k-mer, count) lists computed on the CPU."""
 
-    def __init__(self, fasta: bytes, k: int, m: int, B: int, sequence_type: int = 0):
+    def __init__(self, fasta: bytes, k: int, m: int, B: int, sequence_type: int = 0, threads: int = 1):
         L = lib()
         self.k, self.m = k, m
         self._buf = bytes(fasta)
-        h = L.fko_count(self._buf, len(self._buf), k, m, B, sequence_type)
+        if threads > 1:
+            h = L.fko_count_mt(self._buf, len(self._buf), k, m, B, sequence_type, threads)
+        else:
+            h = L.fko_count(self._buf, len(self._buf), k, m, B, sequence_type)
         if not h:
             raise ValueError(f"invalid oracle parameters k={k} m={m} B={B}")
         self._h = ctypes.c_void_p(h)

@@ -47,6 +47,7 @@
 #include <string.h>
 #include <errno.h>
 #include <sys/stat.h>
+#include <pthread.h>
 
 typedef unsigned __int128 u128;
 
@@ -397,6 +398,119 @@ FKO_API fko_result *fko_count(const uint8_t *fasta, size_t n, int32_t k, int32_t
     for_each_read(fasta, n, map_read, &c);
     for (int32_t b = 0; b < p.B; ++b) reduce_bin(&r->bins[b]);
     free(norm);
+    return r;
+}
+
+/* ------------------------------------------------------------------ */
+/* multi-threaded driver (the CPU baseline; the reference runs Spark    */
+/* local[4], LocalTestKmerCounter.scala:62): the FASTA is cut at record  */
+/* starts into one range per thread (map tasks over input splits), each  */
+/* thread maps its range into private bins, then the bins are merged and */
+/* reduced, bins dealt round-robin over the threads (reduce tasks).      */
+/* Results are identical to fko_count.                                   */
+/* ------------------------------------------------------------------ */
+
+FKO_API void fko_free(fko_result *r);
+
+typedef struct {
+    const uint8_t *buf;
+    size_t lo, hi;
+    fko_params *p;
+    fko_result *part;   /* map: this thread's bins */
+    fko_result *out;    /* reduce: merged bins */
+    fko_result **parts; /* reduce: all threads' bins */
+    int32_t nthreads, tid;
+} mt_task;
+
+static void *mt_map(void *arg) {
+    mt_task *t = (mt_task *)arg;
+    map_ctx c = {t->part, t->p};
+    for_each_read(t->buf + t->lo, t->hi - t->lo, map_read, &c);
+    return NULL;
+}
+
+static void *mt_reduce(void *arg) {
+    mt_task *t = (mt_task *)arg;
+    for (int32_t b = t->tid; b < t->out->nbins; b += t->nthreads) {
+        fko_bin *ob = &t->out->bins[b];
+        int64_t n = 0;
+        for (int32_t j = 0; j < t->nthreads; ++j) n += t->parts[j]->bins[b].n;
+        if (!n) continue;
+        ob->keys = (u128 *)malloc((size_t)n * sizeof(u128));
+        if (!ob->keys) { fprintf(stderr, "fk_oracle: out of memory\n"); abort(); }
+        ob->cap = n;
+        for (int32_t j = 0; j < t->nthreads; ++j) {
+            fko_bin *pb = &t->parts[j]->bins[b];
+            if (pb->n) memcpy(ob->keys + ob->n, pb->keys, (size_t)pb->n * sizeof(u128));
+            ob->n += pb->n;
+            free(pb->keys);
+            pb->keys = NULL;
+            pb->n = 0;
+        }
+        reduce_bin(ob);
+    }
+    return NULL;
+}
+
+FKO_API fko_result *fko_count_mt(const uint8_t *fasta, size_t n, int32_t k, int32_t m, int32_t B,
+                                 int32_t sequence_type, int32_t nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if (k < 1 || k > 64 || m < 1 || m > 15 || m > k || B < 1) return NULL;
+    fko_params p;
+    p.k = k;
+    p.m = m;
+    p.B = fko_clamp_bins(m, B);
+    int32_t *norm = NULL;
+    if (m <= 12) {
+        int64_t sz = (int64_t)1 << (2 * m);
+        norm = (int32_t *)malloc((size_t)sz * sizeof(int32_t));
+        for (int64_t v = 0; v < sz; ++v) norm[v] = fko_norm((int32_t)v, m);
+    }
+    p.norm = norm;
+    /* range starts: thread 0 at 0 (it also skips text before the first
+     * header), the others at the first record start ('>' at a line start)
+     * at or after j*n/T */
+    size_t cut[257];
+    cut[0] = 0;
+    for (int32_t j = 1; j < nthreads; ++j) {
+        size_t q = (size_t)((unsigned __int128)n * (unsigned)j / (unsigned)nthreads);
+        if (q < cut[j - 1]) q = cut[j - 1];
+        while (q < n && !(fasta[q] == '>' && q > 0 && fasta[q - 1] == '\n')) ++q;
+        cut[j] = q;
+    }
+    cut[nthreads] = n;
+    fko_result **parts = (fko_result **)calloc((size_t)nthreads, sizeof(fko_result *));
+    mt_task *tasks = (mt_task *)calloc((size_t)nthreads, sizeof(mt_task));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    fko_result *r = (fko_result *)calloc(1, sizeof(fko_result));
+    r->k = k;
+    r->m = m;
+    r->nbins = p.B;
+    r->bins = (fko_bin *)calloc((size_t)p.B, sizeof(fko_bin));
+    for (int32_t j = 0; j < nthreads; ++j) {
+        parts[j] = (fko_result *)calloc(1, sizeof(fko_result));
+        parts[j]->k = k;
+        parts[j]->m = m;
+        parts[j]->nbins = p.B;
+        parts[j]->bins = (fko_bin *)calloc((size_t)p.B, sizeof(fko_bin));
+        tasks[j] = (mt_task){fasta, cut[j], cut[j + 1], &p, parts[j], r, parts, nthreads, j};
+        pthread_create(&th[j], NULL, mt_map, &tasks[j]);
+    }
+    for (int32_t j = 0; j < nthreads; ++j) pthread_join(th[j], NULL);
+    for (int32_t j = 0; j < nthreads; ++j) {
+        r->total_kmers += parts[j]->total_kmers;
+        r->superkmers += parts[j]->superkmers;
+        r->reads += parts[j]->reads;
+    }
+    for (int32_t j = 0; j < nthreads; ++j) pthread_create(&th[j], NULL, mt_reduce, &tasks[j]);
+    for (int32_t j = 0; j < nthreads; ++j) pthread_join(th[j], NULL);
+    for (int32_t j = 0; j < nthreads; ++j) fko_free(parts[j]);
+    free(parts);
+    free(tasks);
+    free(th);
+    free(norm);
+    (void)sequence_type;
     return r;
 }
 

@@ -149,3 +149,18 @@ def test_oracle_rejects_invalid_params():
         oracle.OracleResult(b">a\nACGT\n", 28, 16, 2048)
     with pytest.raises(ValueError):
         oracle.OracleResult(b">a\nACGT\n", 28, 10, 0)
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8])
+def test_oracle_threads_match_single(threads):
+    # the multi-threaded driver (bench.py's CPU baseline) splits at record starts;
+    # text before the first header, tiny inputs and more threads than records included
+    rng = random.Random(99 + threads)
+    reads = [f">r{i} x\n" + "".join(rng.choice("ACGTN" if rng.random() < 0.1 else "ACGT")
+                                     for _ in range(rng.randint(0, 300))) + "\n" for i in range(300)]
+    for fa in (b"junk\nACGTACGTACGTAC\n" + "".join(reads).encode(), b">a\nACGTACGTACGTACGTACGTACGTACGTAC\n", b""):
+        for k, m, B in ((28, 10, 2048), (21, 7, 64), (55, 12, 8192)):
+            a = oracle.OracleResult(fa, k, m, B)
+            b = oracle.OracleResult(fa, k, m, B, threads=threads)
+            assert (a.total_kmers, a.superkmers, a.reads, a.distinct) == (b.total_kmers, b.superkmers, b.reads, b.distinct)
+            assert a.all_dict() == b.all_dict()
