@@ -150,8 +150,7 @@ template <typename T>
 __device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[4]*/, T *total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T inc = wave_incl_max(v);
-    T exc = __shfl_up(inc, 1, 64);
-    if (lane == 0) exc = ident;
+    const T exc = dpp_move<0x138, 0xf>(ident, inc);  // wave_shr:1 (lane 0 keeps ident)
     if (lane == 63) s_tmp[wid] = inc;
     __syncthreads();
     T off = ident, tot = ident;
