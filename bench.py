@@ -31,7 +31,7 @@ import torch  # noqa: E402  (first: one HIP runtime per process, see fastkmer_am
 import torch.distributed as dist  # noqa: E402
 
 import fastkmer_amd as fk  # noqa: E402
-from fastkmer_amd.exchange import count_distributed  # noqa: E402
+from fastkmer_amd.exchange import RoundCounters, count_distributed, count_distributed_rounds, default_rounds  # noqa: E402
 
 K, M, X, B = 28, 10, 3, 2048
 READ_LEN = 100
@@ -113,6 +113,8 @@ def main() -> None:
     ap.add_argument("--host-input", action="store_true",
                     help="PCIe-inclusive variant: the FASTA starts in pinned host memory and every step "
                          "ingests it (H2D) before counting; reported as a separate metric, never as the headline")
+    ap.add_argument("--rounds", type=int, default=0,
+                    help="N > 1: all-to-all rounds overlapped with the count (0 = auto: 4 up to 4 GPUs, else 2)")
     ap.add_argument("--balance", action="store_true",
                     help="size-aware bin placement (reference useCustomPartitioner=1) instead of bin %% N")
     ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
@@ -144,8 +146,12 @@ def main() -> None:
         seq_type = 1
     rec_bytes = read_len + 14
     n_reads = args.bytes_per_gpu // rec_bytes
-    kc = fk.KmerCounter(k, m, x, b, use_ht=False, sequence_type=seq_type, n_ranks=world, rank=rank,
-                        device=gpu)
+    rounds = 1 if (not distributed or args.balance) else (args.rounds or default_rounds(world))
+    if rounds > 1:  # exchange in overlapped rounds (fastkmer_amd.exchange.RoundCounters)
+        kc = RoundCounters(k, m, x, b, False, seq_type, world=world, rank=rank, rounds=rounds, device=gpu)
+    else:
+        kc = fk.KmerCounter(k, m, x, b, use_ht=False, sequence_type=seq_type, n_ranks=world, rank=rank,
+                            device=gpu)
     if args.workload == "c5":
         # one long record per rank (weak scaling), resident on the device before timing
         n_bases = args.bytes_per_gpu * 60 // 61
@@ -168,7 +174,10 @@ def main() -> None:
         if host_buf is not None:
             kc.ingest_ptr(host_buf.data_ptr(), fasta_bytes)
         if distributed:
-            count_distributed(kc, device=dev, balance=args.balance)
+            if rounds > 1:
+                count_distributed_rounds(kc, device=dev)
+            else:
+                count_distributed(kc, device=dev, balance=args.balance)
         else:
             kc.finish()
 
@@ -233,7 +242,8 @@ def main() -> None:
                        "k": k, "m": m, "x": x, "B": b, "useHT": 0, "sequenceType": seq_type,
                        "fasta_bytes_per_gpu": fasta_bytes,
                        "bases_per_gpu": bases_per_rank, "parallelism": (f"bins placed by size (LPT) over {world} GPU(s)" if args.balance and distributed
-                                           else f"bins round-robin over {world} GPU(s)")},
+                                           else f"bins round-robin over {world} GPU(s)"),
+                       "exchange_rounds": rounds},
             "roofline": {"bound": "hbm",
                          "kernel": "encode+signature stage: k_fasta_parse + k_superkmers (+ their memsets and "
                                    "the per-tile k-mer count scan)",

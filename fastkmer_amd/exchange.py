@@ -84,14 +84,128 @@ def count_distributed(counter, group=None, device=None, balance: bool = False):
     return sum(recv_counts)
 
 
-def execute_job_distributed(configuration, group=None, device=None):
+def default_rounds(world: int) -> int:
+    """Exchange rounds per step: the all-to-all of round r+1 overlaps the count
+    of round r.  With few ranks each peer link carries a large share of the
+    records (N = 2: half of them over one link), so more rounds hide more of
+    the exchange; each extra round costs ~0.3 ms of per-reduce overhead."""
+    return 1 if world <= 1 else (4 if world <= 4 else 2)
+
+
+class RoundCounters:
+    """One rank's bins counted in R exchange rounds.
+
+    R KmerCounter contexts act as virtual ranks rank + world * r of
+    world * R: virtual rank v owns the bins b with b % (world * R) == v, so
+    physical rank (b % world) owns the same bins as the one-round placement
+    and the per-bin results are identical.  parts[0] holds the input and
+    maps it; its emitted send buffer is grouped by virtual destination
+    (round-major), so round r's records for all ranks are one contiguous
+    block.  The result accessors merge the parts.
+    """
+
+    def __init__(self, k, m, x=3, B=2048, use_ht=False, sequence_type=0, world=1, rank=0, rounds=1, device=-1):
+        import fastkmer_amd as fk
+        self.world, self.rank, self.rounds = world, rank, rounds
+        self.parts = [fk.KmerCounter(k, m, x, B, use_ht, sequence_type, n_ranks=world * rounds,
+                                     rank=rank + world * r, device=device) for r in range(rounds)]
+        p0 = self.parts[0]
+        self.k, self.num_bins, self.record_bytes, self.use_ht = p0.k, p0.num_bins, p0.record_bytes, p0.use_ht
+
+    def __getattr__(self, name):  # input side (ingest, synth_device, map, ...) is parts[0]'s
+        if name in ("ingest", "ingest_ptr", "ingest_device", "synth_device", "map", "map_emit", "set_stream"):
+            return getattr(self.parts[0], name)
+        raise AttributeError(name)
+
+    def _part_of(self, b: int):
+        return self.parts[(b % (self.world * self.rounds)) // self.world]
+
+    def bin_sizes(self):
+        out = self.parts[0].bin_sizes()
+        for p in self.parts[1:]:
+            out = out + p.bin_sizes()
+        return out
+
+    def get_bin(self, b: int):
+        return self._part_of(b).get_bin(b)
+
+    def bin_dict(self, b: int) -> dict:
+        return self._part_of(b).bin_dict(b)
+
+    def bin_text(self, b: int) -> str:
+        return self._part_of(b).bin_text(b)
+
+    def write_bins(self, out_dir: str) -> None:
+        for p in self.parts:
+            p.write_bins(out_dir)
+
+    def stats(self) -> dict:
+        st = dict(self.parts[0].stats())
+        for p in self.parts[1:]:
+            q = p.stats()
+            for key in ("records_received", "distinct", "oversize_buckets", "buckets", "ms_partition", "ms_count"):
+                st[key] += q[key]
+        return st
+
+    def close(self) -> None:
+        for p in self.parts:
+            p.close()
+
+
+def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
+    """map -> R overlapped all-to-all rounds -> R reduces for one rank.
+
+    All rounds are posted at once (async); the reduce of round r starts as
+    soon as its records have arrived, while the later rounds are still on the
+    wire.  Returns the number of records received.
+    """
+    world, R = rc.world, rc.rounds
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    host = dist.get_backend(group) == "gloo"
+    wire = torch.device("cpu") if host else dev
+    p0 = rc.parts[0]
+    send_counts = p0.map()  # world * R virtual destinations, round-major
+    total = sum(send_counts)
+    rb = p0.record_bytes
+    send = torch.empty(max(total, 1) * rb, dtype=torch.uint8, device=dev)
+    p0.map_emit(send.data_ptr(), max(total, 1))
+    send = send[: total * rb]
+    payload = send.cpu() if host else send
+    # counts: rank d receives send_counts[r * world + d] for every round r
+    sc = torch.tensor(send_counts, dtype=torch.int64).view(R, world).t().contiguous().view(-1).to(wire)
+    rcv = torch.empty_like(sc)
+    dist.all_to_all_single(rcv, sc, group=group)
+    recv_counts = rcv.view(world, R).t().tolist()  # [round][source]
+    works, recvs, off = [], [], 0
+    for r in range(R):
+        ins = [send_counts[r * world + d] * rb for d in range(world)]
+        outs = [c * rb for c in recv_counts[r]]
+        recv = torch.empty(sum(outs), dtype=torch.uint8, device=wire)
+        works.append(dist.all_to_all_single(recv, payload[off:off + sum(ins)], output_split_sizes=outs,
+                                            input_split_sizes=ins, group=group, async_op=True))
+        recvs.append(recv)
+        off += sum(ins)
+    n = 0
+    for r in range(R):
+        works[r].wait()
+        recv = recvs[r].to(dev) if host else recvs[r]
+        if not host:
+            torch.cuda.current_stream(dev).synchronize()  # round r's records have landed
+        rc.parts[r].reduce(recv.data_ptr(), sum(recv_counts[r]))
+        n += sum(recv_counts[r])
+    return n
+
+
+def execute_job_distributed(configuration, group=None, device=None, rounds=None):
     """SparkBinKmerCounter.executeJob (SBKC:989-1046) for one rank of a job.
 
     Every rank reads the dataset, keeps its shard (fastkmer_amd.sharding),
     maps, exchanges records with the other ranks and counts the bins it owns
     (bin % world == rank); with ``configuration.write`` each rank writes its
     own ``bin<b>`` files into the shared output directory, as the Spark
-    executors do.  Returns the rank's KmerCounter.
+    executors do.  The exchange runs in ``rounds`` overlapped rounds
+    (default_rounds; the size-aware placement uses one).  Returns the rank's
+    counter (a KmerCounter, or a RoundCounters for R > 1).
     """
     import fastkmer_amd as fk
     from fastkmer_amd.sharding import shard_fasta
@@ -102,11 +216,18 @@ def execute_job_distributed(configuration, group=None, device=None):
         data = f.read()
     piece = shard_fasta(data, world, rank, configuration.sequenceType, configuration.k)
     del data
-    kc = fk.KmerCounter(configuration.k, configuration.m, configuration.x, configuration.max_b,
-                        configuration.useHT, configuration.sequenceType, n_ranks=world, rank=rank,
-                        device=dev.index if dev.index is not None else -1)
-    kc.ingest(piece)
-    count_distributed(kc, group=group, device=dev, balance=configuration.useCustomPartitioner)
+    R = 1 if configuration.useCustomPartitioner else (default_rounds(world) if rounds is None else rounds)
+    args = (configuration.k, configuration.m, configuration.x, configuration.max_b, configuration.useHT,
+            configuration.sequenceType)
+    if R > 1:
+        kc = RoundCounters(*args, world=world, rank=rank, rounds=R,
+                           device=dev.index if dev.index is not None else -1)
+        kc.ingest(piece)
+        count_distributed_rounds(kc, group=group, device=dev)
+    else:
+        kc = fk.KmerCounter(*args, n_ranks=world, rank=rank, device=dev.index if dev.index is not None else -1)
+        kc.ingest(piece)
+        count_distributed(kc, group=group, device=dev, balance=configuration.useCustomPartitioner)
     if configuration.write:
         kc.write_bins(configuration.outputDir)
     return kc

@@ -146,12 +146,12 @@ def test_exchange_records_gloo(world, rb):
 
 # ---------------------------------------------------------------- whole job (GPU)
 
-def _job_worker(rank, world, port, cfg_kw):
+def _job_worker(rank, world, port, cfg_kw, rounds=None):
     _init(rank, world, port)
     try:
         from fastkmer_amd.exchange import execute_job_distributed
         torch.cuda.set_device(0)
-        kc = execute_job_distributed(fk.TestConfiguration(**cfg_kw), device=torch.device("cuda", 0))
+        kc = execute_job_distributed(fk.TestConfiguration(**cfg_kw), device=torch.device("cuda", 0), rounds=rounds)
         sizes = kc.bin_sizes()
         if not cfg_kw.get("useCustomPartitioner"):
             assert all(sizes[b] == 0 for b in range(kc.num_bins) if b % world != rank)
@@ -169,16 +169,17 @@ def _read_bins(d: str) -> dict:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("use_ht,seq_type,custom", [(False, 0, False), (True, 0, False), (False, 1, False),
-                                                    (False, 0, True)])
-def test_execute_job_distributed_two_ranks(tmp_path, use_ht, seq_type, custom):
+@pytest.mark.parametrize("use_ht,seq_type,custom,rounds", [(False, 0, False, 1), (False, 0, False, 3),
+                                                           (True, 0, False, None), (False, 1, False, None),
+                                                           (False, 0, True, None)])
+def test_execute_job_distributed_two_ranks(tmp_path, use_ht, seq_type, custom, rounds):
     k, m, B = 28, 10, 512
     data = _long_fasta(40) if seq_type == 1 else fk.synth_fasta(20_000, 100, 200_000, seed=21)
     path = tmp_path / "in.fa"
     path.write_bytes(data)
     cfg = dict(dataset=str(path), outputDirectory=str(tmp_path / "out") + "/", k=k, m=m, x=3, max_b=B,
                sequenceType=seq_type, useHT=use_ht, write=True, useCustomPartitioner=custom)
-    mp.spawn(_job_worker, args=(2, _free_port(), cfg), nprocs=2, join=True)
+    mp.spawn(_job_worker, args=(2, _free_port(), cfg, rounds), nprocs=2, join=True)
     got = _read_bins(fk.TestConfiguration(**cfg).outputDir)
     ref_dir = tmp_path / "ref"
     oracle.OracleResult(data, k, m, B, seq_type).write_bins(str(ref_dir), sorted_eof=not use_ht)
