@@ -8,6 +8,7 @@ Usage: python -m fastkmer_amd.build [--force]
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 
@@ -35,6 +36,53 @@ def _run(cmd: list[str]) -> None:
     subprocess.check_call(cmd)
 
 
+RESOURCES = os.path.join(PKG, "lib", "kernel_resources.txt")
+
+
+def _resource_table(remarks: str) -> list[dict]:
+    """Per-kernel registers / scratch / occupancy / LDS from clang's
+    -Rpass-analysis=kernel-resource-usage remarks."""
+    import re
+    rows, cur = [], None
+    for line in remarks.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = {"kernel": m.group(1)}
+            rows.append(cur)
+            continue
+        m = re.search(r"remark:\s+(VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                      r"LDS Size \[bytes/block\]|VGPRs Spill|SGPRs Spill): (\d+)", line)
+        if m and cur is not None:
+            name = m.group(1)
+            cur[name if "Spill" in name else name.split(" ")[0]] = int(m.group(2))
+    return rows
+
+
+def _compile_kernels(src: str, obj: str) -> None:
+    """Compile the kernel file with resource-usage remarks; no kernel may use
+    scratch (a spilled register array costs a global-memory round trip per
+    access, e.g. 1.57 -> 2.38 ms for the signature kernel)."""
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+           "-Wno-unused-function", "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", obj]
+    print("+", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+    rows = _resource_table(r.stderr)
+    other = "\n".join(l for l in r.stderr.splitlines() if "kernel-resource-usage" not in l and l.strip()
+                      and not l.lstrip().startswith(("|", "^")) and not re.match(r"\s*\d+ \|", l))
+    if other:
+        print(other, file=sys.stderr)
+    if r.returncode != 0:
+        raise subprocess.CalledProcessError(r.returncode, cmd)
+    with open(RESOURCES, "w") as f:
+        f.write("kernel\tVGPRs\tAGPRs\tscratch_B_per_lane\toccupancy_waves_per_SIMD\tLDS_B\n")
+        for row in rows:
+            f.write("\t".join(str(row.get(c, "")) for c in
+                               ("kernel", "VGPRs", "AGPRs", "ScratchSize", "Occupancy", "LDS")) + "\n")
+    bad = [row["kernel"] for row in rows if row.get("ScratchSize", 0) or row.get("VGPRs Spill", 0)]
+    if bad:
+        raise RuntimeError(f"kernels using scratch memory (see {RESOURCES}): {bad}")
+
+
 def build(force: bool = False) -> str:
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     os.makedirs(os.path.dirname(CLI), exist_ok=True)
@@ -43,9 +91,11 @@ def build(force: bool = False) -> str:
         objs = []
         for src in LIB_SOURCES:
             obj = os.path.join(PKG, "lib", os.path.splitext(src)[0] + ".o")
-            lang = ["-x", "hip"] if src.endswith(".cpp") else []
-            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
-                  "-Wall", "-Wno-unused-function", *lang, "-c", os.path.join(CSRC, src), "-o", obj])
+            if src.endswith(".hip"):
+                _compile_kernels(os.path.join(CSRC, src), obj)
+            else:
+                _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+                      "-Wall", "-Wno-unused-function", "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj])
             objs.append(obj)
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
         for o in objs:
