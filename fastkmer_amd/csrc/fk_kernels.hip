@@ -64,7 +64,9 @@ __device__ __forceinline__ T wave_incl_max(T v) {
 }
 
 // exclusive block prefix sum; *total receives the block sum (all threads)
-template <typename T>
+// TRAIL = false drops the closing barrier: only when s_tmp is not written
+// again by the workgroup before every thread has read it (its own array)
+template <typename T, bool TRAIL = true>
 __device__ __forceinline__ T block_excl_sum(T v, T *s_tmp /*[4]*/, T *total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T inc = wave_incl_sum(v);
@@ -77,7 +79,7 @@ __device__ __forceinline__ T block_excl_sum(T v, T *s_tmp /*[4]*/, T *total) {
         if (w < wid) off += x;
         tot += x;
     }
-    __syncthreads();
+    if constexpr (TRAIL) __syncthreads();
     *total = tot;
     return off + inc - v;
 }
@@ -146,7 +148,7 @@ __device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg,
 }
 
 // exclusive block prefix max (identity `ident`)
-template <typename T>
+template <typename T, bool TRAIL = true>
 __device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[4]*/, T *total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T inc = wave_incl_max(v);
@@ -160,7 +162,7 @@ __device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[4]*/, T *t
         if (w < wid) off = x > off ? x : off;
         tot = x > tot ? x : tot;
     }
-    __syncthreads();
+    if constexpr (TRAIL) __syncthreads();
     *total = tot;
     return exc > off ? exc : off;
 }
