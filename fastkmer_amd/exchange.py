@@ -109,6 +109,13 @@ class RoundCounters:
         self.world, self.rank, self.rounds = world, rank, rounds
         self.parts = [fk.KmerCounter(k, m, x, B, use_ht, sequence_type, n_ranks=world * rounds,
                                      rank=rank + world * r, device=device) for r in range(rounds)]
+        # one HIP stream for all R contexts (their work is sequential): with the
+        # RCCL stream and torch's default stream that stays within the 4
+        # hardware queues per process, so the count of round r does not
+        # share a queue with the all-to-all of round r+1
+        self._stream = torch.cuda.Stream(device=device if device >= 0 else None)
+        for p in self.parts:
+            p.set_stream(self._stream.cuda_stream)
         p0 = self.parts[0]
         self.k, self.num_bins, self.record_bytes, self.use_ht = p0.k, p0.num_bins, p0.record_bytes, p0.use_ht
 
@@ -150,6 +157,7 @@ class RoundCounters:
     def close(self) -> None:
         for p in self.parts:
             p.close()
+        self._stream = None
 
 
 def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
