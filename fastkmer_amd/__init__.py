@@ -103,6 +103,10 @@ def lib():
         "fk_record_bytes": (SZ, [P]),
         "fk_map_emit": (ctypes.c_int, [P, P, U64]),
         "fk_reduce": (ctypes.c_int, [P, P, U64]),
+        "fk_set_grouped_emit": (ctypes.c_int, [P, ctypes.c_int32]),
+        "fk_grouped_parts_per_rank": (ctypes.c_int32, [P]),
+        "fk_map_part_counts": (ctypes.c_int, [P, P, P]),
+        "fk_reduce_grouped": (ctypes.c_int, [P, P, U64, P, P, ctypes.c_int32, ctypes.c_int32]),
         "fk_finish": (ctypes.c_int, [P]),
         "fk_num_bins": (I32, [P]),
         "fk_bin_sizes": (ctypes.c_int, [P, P]),
@@ -291,6 +295,31 @@ class KmerCounter:
     def reduce(self, src_ptr: int, n_records: int) -> None:
         self._sizes = None
         _check(lib().fk_reduce(self._h, ctypes.c_void_p(src_ptr), n_records))
+
+    def set_grouped_emit(self, enable: bool = True) -> int:
+        """Group the emitted records by (destination, local bin); returns the
+        parts per destination (fk_set_grouped_emit)."""
+        _check(lib().fk_set_grouped_emit(self._h, 1 if enable else 0))
+        return lib().fk_grouped_parts_per_rank(self._h)
+
+    def map_part_counts(self):
+        """After map() with grouped emit: (records, k-mers) per part, shape [n_ranks, parts]."""
+        parts = lib().fk_grouped_parts_per_rank(self._h)
+        rec = np.zeros(self.n_ranks * parts, dtype=np.uint64)
+        km = np.zeros(self.n_ranks * parts, dtype=np.uint64)
+        _check(lib().fk_map_part_counts(self._h, rec.ctypes.data, km.ctypes.data))
+        return rec.reshape(self.n_ranks, parts), km.reshape(self.n_ranks, parts)
+
+    def reduce_grouped(self, src_ptr: int, n_records: int, seg_records, seg_kmers) -> None:
+        """Count records grouped by sender and local bin (fk_reduce_grouped);
+        seg_records / seg_kmers: [n_senders, parts] arrays."""
+        self._sizes = None
+        sr = np.ascontiguousarray(seg_records, dtype=np.uint64)
+        sk = np.ascontiguousarray(seg_kmers, dtype=np.uint64)
+        if sr.shape != sk.shape or sr.ndim != 2:
+            raise ValueError("seg_records and seg_kmers must be [n_senders, parts] arrays of one shape")
+        _check(lib().fk_reduce_grouped(self._h, ctypes.c_void_p(src_ptr), n_records, sr.ctypes.data, sk.ctypes.data,
+                                       sr.shape[0], sr.shape[1]))
 
     def finish(self) -> None:
         self._sizes = None

@@ -186,6 +186,12 @@ struct fk_ctx {
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
+    // grouped emit (fk_set_grouped_emit): send buffer grouped by (destination, local bin)
+    bool grouped = false;
+    uint32_t grp_nlb = 0;                    // parts per destination = ceil(Bc / n_ranks)
+    DevBuf grp_table;                        // bin -> dest * grp_nlb + bin / n_ranks
+    std::vector<uint64_t> grp_rec, grp_kmer; // per part, after fk_map
+    const uint64_t *rsrc = nullptr;          // records the count stage reads (precs, or d_recv when grouped)
     int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
                                // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
 
@@ -387,7 +393,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
-                      &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk,
+                      &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
@@ -630,7 +636,21 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
 
     // 3a. destination histogram (records per rank)
     c->send_counts.assign(c->G, 0);
-    if (c->G == 1) {
+    if (c->grouped) {
+        // parts = (destination, local bin): the receiver needs no partition pass
+        const uint32_t nparts = c->G * c->grp_nlb;
+        c->grp_rec.assign(nparts, 0);
+        c->grp_kmer.assign(nparts, 0);
+        if (c->nrec) {
+            FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G,
+                              c->grp_table.as<uint32_t>(), nparts, c->ws, s));
+            HIP_TRY(hipMemcpyAsync(c->grp_rec.data(), c->dest.rec.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(c->grp_kmer.data(), c->dest.kmer.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        for (uint32_t d = 0; d < c->G; ++d)
+            for (uint32_t lb = 0; lb < c->grp_nlb; ++lb) c->send_counts[d] += c->grp_rec[(uint64_t)d * c->grp_nlb + lb];
+    } else if (c->G == 1) {
         c->send_counts[0] = c->nrec;
     } else if (c->nrec) {
         FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, owner_table(c), c->G, c->ws, s));
@@ -652,7 +672,10 @@ FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
     if (!c->nrec) return FK_OK;
     const double t0 = now_ms();
     hipStream_t s = c->stream;
-    if (c->G == 1) {
+    if (c->grouped) {
+        FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, c->grp_table.as<uint32_t>(),
+                            (uint64_t *)d_send, s));
+    } else if (c->G == 1) {
         HIP_TRY(hipMemcpyAsync(d_send, c->records.p, c->nrec * c->W * 8, hipMemcpyDeviceToDevice, s));
     } else {
         FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, owner_table(c), (uint64_t *)d_send, s));
@@ -779,13 +802,13 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         FK_TRY(ensure(c->lp, ((uint64_t)nchunks << F1) * 4));
         FK_TRY(ensure(c->sc_total, nsc_all * 8));
         HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
-        HIP_TRY(launch_expand_hist_sc(c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F, F2,
+        HIP_TRY(launch_expand_hist_sc(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F, F2,
                                       c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
         HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F1, c->lp.as<uint32_t>(),
                                    c->sc_total.as<uint64_t>(), s));
     } else {
         FK_TRY(ensure(c->lp, (uint64_t)nchunks * ncell * 4));
-        HIP_TRY(launch_expand_hist(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+        HIP_TRY(launch_expand_hist(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,
                                    c->lp.as<uint32_t>(), s));
         HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
                                    c->cell_total.as<uint64_t>(), s));
@@ -807,11 +830,11 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     }
     if (two_level) {
         FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
-        HIP_TRY(launch_expand_two_level(c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
+        HIP_TRY(launch_expand_two_level(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
                                         F2, c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->mid.as<uint64_t>(),
                                         c->keys.as<uint64_t>(), s));
     } else {
-        HIP_TRY(launch_expand_scatter(c->W, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, k, F,
+        HIP_TRY(launch_expand_scatter(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,
                                       c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
                                       max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
     }
@@ -938,7 +961,7 @@ static int reduce_ht(fk_ctx *c, uint32_t nchunks, const std::vector<uint64_t> &b
     HIP_TRY(hipMemsetAsync(c->tcounts.p, 0, nslots * 4, s));
     if (c->KW == 2) HIP_TRY(hipMemsetAsync(c->tstate.p, 0, nslots * 4, s));
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
-    HIP_TRY(launch_ht_insert(c->W, c->KW, c->precs.as<uint64_t>(), c->chunks.as<Chunk>(), nchunks, c->cfg.k,
+    HIP_TRY(launch_ht_insert(c->W, c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->cfg.k,
                              c->table_off.as<uint64_t>(), c->tkeys.as<uint64_t>(), c->tstate.as<uint32_t>(),
                              c->tcounts.as<uint32_t>(), c->misc.as<unsigned long long>(), s));
     HIP_TRY(launch_ht_flags(c->tcounts.as<uint32_t>(), nslots, c->flags.as<uint32_t>(), s));
@@ -961,52 +984,39 @@ static int reduce_ht(fk_ctx *c, uint32_t nchunks, const std::vector<uint64_t> &b
     return FK_OK;
 }
 
-FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
-    if (!c) return set_err(FK_E_INVALID, "null ctx");
-    if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
-    const double t0 = now_ms();
-    hipStream_t s = c->stream;
-    c->have_result = false;
-    const uint32_t nlb = c->nlb;
-    HIP_TRY(hipEventRecord(c->ev[4], s));
-    FK_TRY(part_count(c->part, c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, local_table(c), nlb, c->ws, s));
-    std::vector<uint64_t> brec(nlb), bkm(nlb);
-    if (nlb) {
-        HIP_TRY(hipMemcpyAsync(brec.data(), c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(bkm.data(), c->part.kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipStreamSynchronize(s));
-    // record offsets per local bin and chunk table (chunks never span bins)
-    std::vector<uint64_t> roff(nlb + 1, 0);
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> bcb(nlb + 1, 0);
-    uint64_t total_kmers = 0, max_bin = 0;
+// Chunks of <= CHUNK_RECORDS records per local bin (chunks never span bins;
+// a bin's chunks are consecutive).  ranges[lb] = the bin's record ranges.
+static void build_chunks(uint32_t nlb, const std::vector<std::vector<std::pair<uint64_t, uint64_t>>> &ranges,
+                         std::vector<Chunk> &chunks, std::vector<uint32_t> &bcb) {
+    chunks.clear();
+    bcb.assign((size_t)nlb + 1, 0);
     for (uint32_t lb = 0; lb < nlb; ++lb) {
-        roff[lb + 1] = roff[lb] + brec[lb];
-        total_kmers += bkm[lb];
-        max_bin = std::max(max_bin, bkm[lb]);
         bcb[lb] = (uint32_t)chunks.size();
-        for (uint64_t r = roff[lb]; r < roff[lb + 1]; r += CHUNK_RECORDS) {
-            Chunk ch;
-            ch.rec_begin = r;
-            ch.rec_end = std::min<uint64_t>(r + CHUNK_RECORDS, roff[lb + 1]);
-            ch.lbin = lb;
-            ch.pad = 0;
-            chunks.push_back(ch);
+        for (const auto &rg : ranges[lb]) {
+            for (uint64_t r = rg.first; r < rg.second; r += CHUNK_RECORDS) {
+                Chunk ch;
+                ch.rec_begin = r;
+                ch.rec_end = std::min<uint64_t>(r + CHUNK_RECORDS, rg.second);
+                ch.lbin = lb;
+                ch.pad = 0;
+                chunks.push_back(ch);
+            }
         }
     }
     bcb[nlb] = (uint32_t)chunks.size();
+}
+
+// The count over the chunk table (records at c->rsrc), bin offsets, stats.
+static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chunks, const std::vector<uint32_t> &bcb,
+                       const std::vector<uint64_t> &bkm, double t0) {
+    hipStream_t s = c->stream;
+    const uint32_t nlb = c->nlb;
     const uint32_t nchunks = (uint32_t)chunks.size();
-    if (roff[nlb] != nrecv)
-        return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
-                       (unsigned long long)roff[nlb], (unsigned long long)nrecv);
-    FK_TRY(ensure(c->precs, nrecv * c->W * 8));
-    FK_TRY(ensure(c->chunks, nchunks * sizeof(Chunk)));
-    FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)nlb + 1) * 4));
-    if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), (nlb + 1) * 4, hipMemcpyHostToDevice, s));
-    FK_TRY(part_scatter(c->part, c->W, (const uint64_t *)d_recv, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
-    HIP_TRY(hipEventRecord(c->ev[5], s));
+    uint64_t total_kmers = 0, max_bin = 0;
+    for (uint32_t lb = 0; lb < nlb; ++lb) {
+        total_kmers += bkm[lb];
+        max_bin = std::max(max_bin, bkm[lb]);
+    }
     HIP_TRY(hipEventRecord(c->ev[6], s));
     if (c->cfg.use_ht)
         FK_TRY(reduce_ht(c, nchunks, bkm));
@@ -1023,6 +1033,117 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     c->stats.ms_total += now_ms() - t0;
     c->have_result = true;
     return FK_OK;
+}
+
+static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std::vector<uint32_t> &bcb) {
+    hipStream_t s = c->stream;
+    const uint32_t nchunks = (uint32_t)chunks.size();
+    FK_TRY(ensure(c->chunks, nchunks * sizeof(Chunk)));
+    FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)c->nlb + 1) * 4));
+    if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), ((uint64_t)c->nlb + 1) * 4, hipMemcpyHostToDevice, s));
+    return FK_OK;
+}
+
+FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
+    const double t0 = now_ms();
+    hipStream_t s = c->stream;
+    c->have_result = false;
+    const uint32_t nlb = c->nlb;
+    HIP_TRY(hipEventRecord(c->ev[4], s));
+    FK_TRY(part_count(c->part, c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, local_table(c), nlb, c->ws, s));
+    std::vector<uint64_t> brec(nlb), bkm(nlb);
+    if (nlb) {
+        HIP_TRY(hipMemcpyAsync(brec.data(), c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(bkm.data(), c->part.kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    // record offsets per local bin after the partition
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
+    uint64_t off = 0;
+    for (uint32_t lb = 0; lb < nlb; ++lb) {
+        ranges[lb].push_back({off, off + brec[lb]});
+        off += brec[lb];
+    }
+    if (off != nrecv)
+        return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
+                       (unsigned long long)off, (unsigned long long)nrecv);
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    build_chunks(nlb, ranges, chunks, bcb);
+    FK_TRY(ensure(c->precs, nrecv * c->W * 8));
+    FK_TRY(upload_chunks(c, chunks, bcb));
+    FK_TRY(part_scatter(c->part, c->W, (const uint64_t *)d_recv, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
+    HIP_TRY(hipEventRecord(c->ev[5], s));
+    c->rsrc = c->precs.as<uint64_t>();
+    return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
+}
+
+FK_EXPORT int fk_set_grouped_emit(fk_ctx *c, int32_t enable) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (enable && c->custom_owners)
+        return set_err(FK_E_STATE, "grouped emit needs the default placement (bin %% n_ranks)");
+    c->grouped = enable != 0;
+    c->mapped = false;
+    if (!c->grouped) return FK_OK;
+    c->grp_nlb = (uint32_t)((c->Bc + (int)c->G - 1) / (int)c->G);
+    std::vector<uint32_t> table((size_t)c->Bc);
+    for (int32_t b = 0; b < c->Bc; ++b) table[b] = ((uint32_t)b % c->G) * c->grp_nlb + (uint32_t)b / c->G;
+    FK_TRY(ensure(c->grp_table, (uint64_t)c->Bc * 4));
+    HIP_TRY(hipMemcpy(c->grp_table.p, table.data(), (uint64_t)c->Bc * 4, hipMemcpyHostToDevice));
+    return FK_OK;
+}
+
+FK_EXPORT int32_t fk_grouped_parts_per_rank(const fk_ctx *c) { return c && c->grouped ? (int32_t)c->grp_nlb : 0; }
+
+FK_EXPORT int fk_map_part_counts(fk_ctx *c, uint64_t *records, uint64_t *kmers) {
+    if (!c || !records || !kmers) return set_err(FK_E_INVALID, "null argument");
+    if (!c->grouped || !c->mapped) return set_err(FK_E_STATE, "fk_map_part_counts needs fk_set_grouped_emit and fk_map");
+    std::copy(c->grp_rec.begin(), c->grp_rec.end(), records);
+    std::copy(c->grp_kmer.begin(), c->grp_kmer.end(), kmers);
+    return FK_OK;
+}
+
+FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, const uint64_t *seg_records,
+                                const uint64_t *seg_kmers, int32_t nseg, int32_t parts_per_seg) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
+    if (nseg < 0 || parts_per_seg < 0 || (nseg && (!seg_records || !seg_kmers)))
+        return set_err(FK_E_INVALID, "bad segment table");
+    const double t0 = now_ms();
+    hipStream_t s = c->stream;
+    c->have_result = false;
+    const uint32_t nlb = c->nlb;
+    if ((uint32_t)parts_per_seg < nlb) return set_err(FK_E_INVALID, "%d parts per segment < %u local bins",
+                                                      parts_per_seg, nlb);
+    HIP_TRY(hipEventRecord(c->ev[4], s));
+    // segment s holds, bin after bin, seg_records[s * parts + lb] records of local bin lb
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
+    std::vector<uint64_t> bkm(nlb, 0);
+    uint64_t off = 0;
+    for (int32_t sg = 0; sg < nseg; ++sg) {
+        for (int32_t lb = 0; lb < parts_per_seg; ++lb) {
+            const uint64_t n = seg_records[(uint64_t)sg * parts_per_seg + lb];
+            if (n && (uint32_t)lb >= nlb) return set_err(FK_E_INVALID, "records for local bin %d of %u", lb, nlb);
+            if (n) {
+                ranges[lb].push_back({off, off + n});
+                bkm[lb] += seg_kmers[(uint64_t)sg * parts_per_seg + lb];
+            }
+            off += n;
+        }
+    }
+    if (off != nrecv)
+        return set_err(FK_E_INVALID, "segment table holds %llu records, buffer %llu", (unsigned long long)off,
+                       (unsigned long long)nrecv);
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    build_chunks(nlb, ranges, chunks, bcb);
+    FK_TRY(upload_chunks(c, chunks, bcb));
+    HIP_TRY(hipEventRecord(c->ev[5], s));
+    c->rsrc = (const uint64_t *)d_recv;
+    return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
 }
 
 FK_EXPORT int fk_finish(fk_ctx *c) {

@@ -117,6 +117,9 @@ class RoundCounters:
         for p in self.parts:
             p.set_stream(self._stream.cuda_stream)
         p0 = self.parts[0]
+        # the sender groups its records by (virtual destination, local bin), so
+        # the receiving contexts skip their partition pass (fk_reduce_grouped)
+        self.parts_per_rank = p0.set_grouped_emit(True)
         self.k, self.num_bins, self.record_bytes, self.use_ht = p0.k, p0.num_bins, p0.record_bytes, p0.use_ht
 
     def __getattr__(self, name):  # input side (ingest, synth_device, map, ...) is parts[0]'s
@@ -171,19 +174,24 @@ def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     host = dist.get_backend(group) == "gloo"
     wire = torch.device("cpu") if host else dev
+    import numpy as np
     p0 = rc.parts[0]
     send_counts = p0.map()  # world * R virtual destinations, round-major
+    prec, pkm = p0.map_part_counts()  # [world * R, parts]: records / k-mers per (destination, local bin)
+    parts = prec.shape[1]
     total = sum(send_counts)
     rb = p0.record_bytes
     send = torch.empty(max(total, 1) * rb, dtype=torch.uint8, device=dev)
     p0.map_emit(send.data_ptr(), max(total, 1))
     send = send[: total * rb]
     payload = send.cpu() if host else send
-    # counts: rank d receives send_counts[r * world + d] for every round r
-    sc = torch.tensor(send_counts, dtype=torch.int64).view(R, world).t().contiguous().view(-1).to(wire)
+    # per-part counts: rank d receives the rows of virtual ranks r * world + d, every round r
+    tab = np.stack([prec, pkm], axis=1).astype(np.int64).reshape(R, world, 2, parts).transpose(1, 0, 2, 3)
+    sc = torch.from_numpy(np.ascontiguousarray(tab)).reshape(-1).to(wire)
     rcv = torch.empty_like(sc)
     dist.all_to_all_single(rcv, sc, group=group)
-    recv_counts = rcv.view(world, R).t().tolist()  # [round][source]
+    rt = rcv.cpu().numpy().reshape(world, R, 2, parts)  # [source][round][records | k-mers][local bin]
+    recv_counts = [[int(rt[src, r, 0].sum()) for src in range(world)] for r in range(R)]  # [round][source]
     works, recvs, off = [], [], 0
     for r in range(R):
         ins = [send_counts[r * world + d] * rb for d in range(world)]
@@ -199,7 +207,7 @@ def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
         recv = recvs[r].to(dev) if host else recvs[r]
         if not host:
             torch.cuda.current_stream(dev).synchronize()  # round r's records have landed
-        rc.parts[r].reduce(recv.data_ptr(), sum(recv_counts[r]))
+        rc.parts[r].reduce_grouped(recv.data_ptr(), sum(recv_counts[r]), rt[:, r, 0, :], rt[:, r, 1, :])
         n += sum(recv_counts[r])
     return n
 

@@ -118,6 +118,19 @@ int fk_map_emit(fk_ctx *ctx, void *d_send, uint64_t cap_records);
 /* Reduce side (reduceByKey + extractKXmers[HT]): count the records in
  * d_recv (device memory, fk_record_bytes each, all owned by this rank). */
 int fk_reduce(fk_ctx *ctx, const void *d_recv, uint64_t n_records);
+/* Grouped exchange (default placement only): with fk_set_grouped_emit(ctx, 1)
+ * before fk_map, fk_map_emit groups the records by (destination rank, local
+ * bin) -- the reduceByKey grouping of SBKC:1035 done on the sender -- and
+ * fk_map_part_counts returns records / k-mers per part ([n_ranks][parts],
+ * parts = fk_grouped_parts_per_rank).  A receiver then skips its partition
+ * pass: fk_reduce_grouped counts d_recv = n_seg segments (one per sender, in
+ * order), each holding seg_records[s * parts + lb] records of local bin lb,
+ * bin after bin. */
+int fk_set_grouped_emit(fk_ctx *ctx, int32_t enable);
+int32_t fk_grouped_parts_per_rank(const fk_ctx *ctx);
+int fk_map_part_counts(fk_ctx *ctx, uint64_t *records, uint64_t *kmers);
+int fk_reduce_grouped(fk_ctx *ctx, const void *d_recv, uint64_t n_records, const uint64_t *seg_records,
+                      const uint64_t *seg_kmers, int32_t n_seg, int32_t parts_per_seg);
 /* Single rank: fk_map + fk_reduce on the local records. */
 int fk_finish(fk_ctx *ctx);
 

@@ -436,3 +436,54 @@ def test_parse_line_lookback_paths_vs_oracle(monkeypatch, case):
         ref = oracle.OracleResult(fasta, k, m, 512)
         assert kc.stats()["kmers"] == ref.total_kmers
         assert_same_as_oracle(kc, ref)
+
+
+@pytest.mark.parametrize("k,m,B,use_ht", [(28, 10, 2048, False), (28, 10, 2048, True), (55, 12, 8192, False)])
+def test_grouped_exchange_in_one_process_matches_oracle(k, m, B, use_ht):
+    # fk_set_grouped_emit / fk_reduce_grouped: senders group records by
+    # (destination, local bin); receivers count the segments without a partition pass
+    fasta = fk.synth_fasta(20_000, 150 if k > 32 else 100, 300_000, seed=13)
+    G = 3
+    rec = len(fasta) // 20_000
+    shards = [fasta[r * rec * 6667:(r + 1) * rec * 6667] if r < G - 1 else fasta[r * rec * 6667:]
+              for r in range(G)]
+    ranks = [fk.KmerCounter(k, m, 3, B, use_ht, 0, n_ranks=G, rank=r) for r in range(G)]
+    import torch
+    sends = []
+    for r in range(G):
+        parts = ranks[r].set_grouped_emit(True)
+        ranks[r].ingest(shards[r])
+        counts = ranks[r].map()
+        prec, pkm = ranks[r].map_part_counts()
+        assert prec.shape == (G, parts) and [int(x) for x in prec.sum(axis=1)] == counts
+        buf = torch.empty(max(sum(counts), 1) * ranks[r].record_bytes, dtype=torch.uint8, device="cuda")
+        ranks[r].map_emit(buf.data_ptr(), max(sum(counts), 1))
+        torch.cuda.synchronize()
+        sends.append((buf, counts, prec, pkm))
+    rb = ranks[0].record_bytes
+    for dst in range(G):
+        pieces, seg_rec, seg_km = [], [], []
+        for src in range(G):
+            buf, counts, prec, pkm = sends[src]
+            off = sum(counts[:dst])
+            pieces.append(buf[off * rb:(off + counts[dst]) * rb])
+            seg_rec.append(prec[dst])
+            seg_km.append(pkm[dst])
+        recv = torch.cat(pieces)
+        ranks[dst].reduce_grouped(recv.data_ptr(), recv.numel() // rb, np.stack(seg_rec), np.stack(seg_km))
+        torch.cuda.synchronize()
+    ref = oracle.OracleResult(fasta, k, m, B)
+    total = np.zeros(ref.nbins, dtype=np.int64)
+    for dst in range(G):
+        sizes = ranks[dst].bin_sizes().astype(np.int64)
+        assert all(sizes[b] == 0 for b in range(ref.nbins) if b % G != dst)
+        total += sizes
+    assert np.array_equal(total, ref.bin_sizes())
+    for b in range(0, ref.nbins, 37):
+        if ref.bin_size(b):
+            hi, lo, cnt = counter_arrays(ranks[b % G], b)
+            rhi, rlo, rcnt = ref.bin_arrays(b)
+            if use_ht:
+                o = np.lexsort((lo, hi))
+                hi, lo, cnt = hi[o], lo[o], cnt[o]
+            assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
