@@ -18,7 +18,8 @@
 namespace fk {
 
 constexpr int ENC_TILE = 16384;  // FASTA bytes per parse/encode workgroup
-constexpr int SIG_TILE = 4096;   // k-mer start positions per signature workgroup (256 x 16)
+constexpr int SIG_NT = 512;      // threads per signature workgroup
+constexpr int SIG_TILE = SIG_NT * 16;  // k-mer start positions per signature workgroup
 constexpr int SIG_PPT = 16;      // positions per thread == max k-mers per record
 constexpr int POS_PAD_WORDS = 64;  // zero words after the packed stream (halo reads)
 constexpr int SORT_CAP = 4096;   // keys per LDS-sorted bucket (u64 keys; half for 128-bit keys)

@@ -66,15 +66,15 @@ __device__ __forceinline__ T wave_incl_max(T v) {
 // exclusive block prefix sum; *total receives the block sum (all threads)
 // TRAIL = false drops the closing barrier: only when s_tmp is not written
 // again by the workgroup before every thread has read it (its own array)
-template <typename T, bool TRAIL = true>
-__device__ __forceinline__ T block_excl_sum(T v, T *s_tmp /*[4]*/, T *total) {
+template <typename T, bool TRAIL = true, int NTH = NT>
+__device__ __forceinline__ T block_excl_sum(T v, T *s_tmp /*[NTH / 64]*/, T *total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T inc = wave_incl_sum(v);
     if (lane == 63) s_tmp[wid] = inc;
     __syncthreads();
     T off = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) {
+    for (int w = 0; w < NTH / 64; ++w) {
         T x = s_tmp[w];
         if (w < wid) off += x;
         tot += x;
@@ -148,8 +148,8 @@ __device__ uint64_t lookback_excl(uint64_t *status, uint64_t tile, uint64_t agg,
 }
 
 // exclusive block prefix max (identity `ident`)
-template <typename T, bool TRAIL = true>
-__device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[4]*/, T *total) {
+template <typename T, bool TRAIL = true, int NTH = NT>
+__device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[NTH / 64]*/, T *total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T inc = wave_incl_max(v);
     const T exc = dpp_move<0x138, 0xf>(ident, inc);  // wave_shr:1 (lane 0 keeps ident)
@@ -157,7 +157,7 @@ __device__ __forceinline__ T block_excl_max(T v, T ident, T *s_tmp /*[4]*/, T *t
     __syncthreads();
     T off = ident, tot = ident;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) {
+    for (int w = 0; w < NTH / 64; ++w) {
         T x = s_tmp[w];
         if (w < wid) off = x > off ? x : off;
         tot = x > tot ? x : tot;
