@@ -17,7 +17,8 @@
 
 namespace fk {
 
-constexpr int ENC_TILE = 16384;  // FASTA bytes per parse/encode workgroup
+constexpr int ENC_NT = 512;      // threads per parse/encode workgroup
+constexpr int ENC_TILE = ENC_NT * 64;  // FASTA bytes per parse/encode workgroup (64 per thread)
 constexpr int SIG_NT = 512;      // threads per signature workgroup
 constexpr int SIG_TILE = SIG_NT * 16;  // k-mer start positions per signature workgroup
 constexpr int SIG_PPT = 16;      // positions per thread == max k-mers per record
