@@ -208,13 +208,32 @@ __global__ __launch_bounds__(NT) void k_scan_down(const TI *in, TO *out, uint64_
                                                   Op op, TO *total) {
     __shared__ TO s_tmp[NT / 64];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_SEG + (uint64_t)threadIdx.x * SCAN_IPT;
+    static_assert(sizeof(TI) * SCAN_IPT % 16 == 0 && sizeof(TO) * SCAN_IPT % 16 == 0, "16-B segments");
+    // a thread owns SCAN_IPT consecutive elements: 16-B loads and stores when
+    // its segment is whole and both arrays are 16-B aligned (scalar accesses
+    // at a 32-64 B lane stride touch every line SCAN_IPT times)
+    const bool vec = base + SCAN_IPT <= n && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
     TO v[SCAN_IPT];
     TO acc = ident;
+    if (vec) {
+        union {
+            TI t[SCAN_IPT];
+            uint4 q[sizeof(TI) * SCAN_IPT / 16];
+        } u;
 #pragma unroll
-    for (int i = 0; i < SCAN_IPT; ++i) {
-        uint64_t idx = base + i;
-        v[i] = idx < n ? (TO)in[idx] : ident;
-        acc = op(acc, v[i]);
+        for (int i = 0; i < (int)(sizeof(TI) * SCAN_IPT / 16); ++i) u.q[i] = reinterpret_cast<const uint4 *>(in + base)[i];
+#pragma unroll
+        for (int i = 0; i < SCAN_IPT; ++i) {
+            v[i] = (TO)u.t[i];
+            acc = op(acc, v[i]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_IPT; ++i) {
+            uint64_t idx = base + i;
+            v[i] = idx < n ? (TO)in[idx] : ident;
+            acc = op(acc, v[i]);
+        }
     }
     TO tot;
     TO pre;
@@ -224,11 +243,25 @@ __global__ __launch_bounds__(NT) void k_scan_down(const TI *in, TO *out, uint64_
         pre = block_excl_sum<TO>(acc, s_tmp, &tot);
     }
     TO run = op(carry ? carry[blockIdx.x] : ident, pre);
+    if (vec) {
+        union {
+            TO t[SCAN_IPT];
+            uint4 q[sizeof(TO) * SCAN_IPT / 16];
+        } u;
 #pragma unroll
-    for (int i = 0; i < SCAN_IPT; ++i) {
-        uint64_t idx = base + i;
-        if (idx < n) out[idx] = run;
-        run = op(run, v[i]);
+        for (int i = 0; i < SCAN_IPT; ++i) {
+            u.t[i] = run;
+            run = op(run, v[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(TO) * SCAN_IPT / 16); ++i) reinterpret_cast<uint4 *>(out + base)[i] = u.q[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_IPT; ++i) {
+            uint64_t idx = base + i;
+            if (idx < n) out[idx] = run;
+            run = op(run, v[i]);
+        }
     }
     if (total && threadIdx.x == NT - 1 && blockIdx.x == gridDim.x - 1) *total = run;
 }
