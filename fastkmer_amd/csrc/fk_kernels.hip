@@ -183,9 +183,9 @@ struct OpMax {
     __device__ T operator()(T a, T b) const { return a > b ? a : b; }
 };
 
-template <typename TI, typename TO, typename Op>
+template <typename TI, typename TO, typename Op, bool IS_MAX>
 __global__ __launch_bounds__(NT) void k_scan_reduce(const TI *in, uint64_t n, TO *sums, TO ident, Op op) {
-    __shared__ TO s_red[NT];
+    __shared__ TO s_tmp[NT / 64];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_SEG;
     TO acc = ident;
 #pragma unroll
@@ -193,13 +193,13 @@ __global__ __launch_bounds__(NT) void k_scan_reduce(const TI *in, uint64_t n, TO
         uint64_t idx = base + (uint64_t)i * NT + threadIdx.x;
         if (idx < n) acc = op(acc, (TO)in[idx]);
     }
-    s_red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = NT / 2; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) s_red[threadIdx.x] = op(s_red[threadIdx.x], s_red[threadIdx.x + st]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) sums[blockIdx.x] = s_red[0];
+    // wave reductions + one barrier (the block scans' totals), not an LDS tree
+    TO tot;
+    if constexpr (IS_MAX)
+        (void)block_excl_max<TO, false>(acc, ident, s_tmp, &tot);
+    else
+        (void)block_excl_sum<TO, false>(acc, s_tmp, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
 // exclusive scan of one segment with a carry-in (carry[blockIdx] or ident)
@@ -281,7 +281,7 @@ static hipError_t scan_impl(const TI *in, TO *out, uint64_t n, TO ident, TO *tot
     if (ws_bytes < 2 * nb * sizeof(TO)) return hipErrorOutOfMemory;
     TO *sums = (TO *)ws;
     TO *sums_scan = sums + nb;
-    k_scan_reduce<TI, TO, Op><<<(unsigned)nb, NT, 0, s>>>(in, n, sums, ident, Op());
+    k_scan_reduce<TI, TO, Op, IS_MAX><<<(unsigned)nb, NT, 0, s>>>(in, n, sums, ident, Op());
     hipError_t e = scan_impl<TO, TO, Op, IS_MAX>(sums, sums_scan, nb, ident, (TO *)nullptr,
                                                  (char *)(sums_scan + nb), ws_bytes - 2 * nb * sizeof(TO), s);
     if (e != hipSuccess) return e;
