@@ -51,7 +51,7 @@ class fk_stats(ctypes.Structure):
                  "oversize_buckets", "buckets", "fine_bits")] + \
                [(n, ctypes.c_double) for n in
                 ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
-                 "ms_signature_kernel")]
+                 "ms_signature_kernel")] + [("fused_map", ctypes.c_uint64)]
 
 
 _lib = None

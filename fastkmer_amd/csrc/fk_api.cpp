@@ -158,6 +158,30 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Every exported call that touches the GPU selects the context's device for
+// its duration and restores the caller's current device on return, so one
+// thread may drive contexts on several GPUs and a context may move between
+// threads (e.g. JNI executor threads).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+        }
+        if (dev >= 0 && prev != dev) {
+            (void)hipSetDevice(dev);
+        } else {
+            prev = -1;  // nothing to restore
+        }
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 constexpr uint32_t CHUNK_RECORDS = 16384;  // records per expansion workgroup (never spans two bins)
 
 }  // namespace
@@ -186,6 +210,9 @@ struct fk_ctx {
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
+    int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
+    int fused_nt = 512;        // FASTKMER_FUSED_NT: threads per fused map workgroup (256 or 512)
+    bool last_map_fused = false;  // the last fk_map used the fused kernel (stats, tests)
     // grouped emit (fk_set_grouped_emit): send buffer grouped by (destination, local bin)
     bool grouped = false;
     uint32_t grp_nlb = 0;                    // parts per destination = ceil(Bc / n_ranks)
@@ -357,6 +384,10 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (bp && bp[0]) c->wave_bpw = atoi(bp);
     const char *pl = getenv("FASTKMER_PARSE_LOOKBACK");
     if (pl && pl[0]) c->parse_scan = atoi(pl) == 0;
+    const char *fu = getenv("FASTKMER_FUSED");
+    if (fu && fu[0]) c->fused = atoi(fu);
+    const char *fn = getenv("FASTKMER_FUSED_NT");
+    if (fn && fn[0]) c->fused_nt = atoi(fn) == 256 ? 256 : 512;
     const char *cm = getenv("FASTKMER_COUNT_MODE");
     if (cm && cm[0]) c->count_mode = atoi(cm);
     if (cfg->device >= 0) {
@@ -364,13 +395,19 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
             delete c;
             return set_err(FK_E_DEVICE, "device %d out of range (%d devices)", cfg->device, ndev);
         }
-        e = hipSetDevice(cfg->device);
-        if (e != hipSuccess) {
+        c->device = cfg->device;
+    } else {
+        (void)hipGetDevice(&c->device);
+    }
+    DeviceGuard dg_(c->device);  // the caller's current device is restored on return
+    {
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess || cur != c->device) {
+            (void)hipGetLastError();
             delete c;
-            return set_err(FK_E_DEVICE, "hipSetDevice(%d): %s", cfg->device, hipGetErrorString(e));
+            return set_err(FK_E_DEVICE, "cannot select device %d", c->device);
         }
     }
-    (void)hipGetDevice(&c->device);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -390,6 +427,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 
 FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (!c) return;
+    DeviceGuard dg_(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
@@ -418,6 +456,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
 
 FK_EXPORT int fk_set_stream(fk_ctx *c, void *s) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
     if (c->own_stream && c->stream) {
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamDestroy(c->stream);
@@ -446,8 +485,13 @@ constexpr size_t PIN_CHUNK = 64ull << 20;  // pinned staging buffer (x2) for pag
 FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     (void)last;
     if (!c || (!fasta && n)) return set_err(FK_E_INVALID, "null argument");
-    if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>())
-        return set_err(FK_E_STATE, "fk_ingest after fk_ingest_device on the same job");
+    DeviceGuard dg_(c->device);
+    if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>()) {
+        // a borrowed device input (fk_ingest_device): host chunks cannot be appended
+        // to it, but a host ingest that starts a new job replaces it
+        if (!c->ingest_fresh) return set_err(FK_E_STATE, "fk_ingest appending to an fk_ingest_device input");
+        c->d_fasta = nullptr;
+    }
     hipStream_t s = c->stream;
     if (c->ingest_fresh || !c->d_fasta) {
         c->n_fasta = 0;
@@ -495,6 +539,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
 FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
     (void)last;
     if (!c || (!d && n)) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
     c->ingest_fresh = true;
     reset_results(c);
     if (((uintptr_t)d & 15) != 0) {
@@ -511,6 +556,7 @@ FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
 FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_reads, int32_t read_len,
                                     uint64_t genome_len, uint64_t seed, double err_rate, double n_rate) {
     if (!c || read_len < 1 || genome_len < 1) return set_err(FK_E_INVALID, "bad synth arguments");
+    DeviceGuard dg_(c->device);
     const SynthParams p = make_synth(first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate);
     const uint64_t nb = n_reads * p.rec_bytes;
     FK_TRY(ensure(c->fasta_own, nb));
@@ -542,8 +588,52 @@ static int32_t global_bin(const fk_ctx *c, uint32_t lb) {
     return c->custom_owners ? c->h_lbin_bin[lb] : (int32_t)(c->cfg.rank + lb * c->G);
 }
 
+// Fused parse + signature (k_map_fused): FASTA bytes to records in one kernel.
+// *ok = false when a tile raised the fallback flag (the caller then maps with
+// the two-kernel path, which places every input).
+static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
+    hipStream_t s = c->stream;
+    *ok = false;
+    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    const uint64_t ntiles = (n + tile - 1) / tile;
+    FK_TRY(ensure(c->sig_status, ntiles * 8));
+    FK_TRY(ensure(c->counters, 64));
+    uint64_t rec_cap = std::max<uint64_t>(n / 6, 4096);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        FK_TRY(ensure(c->records, rec_cap * c->W * 8));
+        rec_cap = c->records.bytes / (c->W * 8);
+        HIP_TRY(hipEventRecord(c->ev[2], s));
+        HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
+        HIP_TRY(hipMemsetAsync(c->sig_status.p, 0, ntiles * 8, s));
+        HIP_TRY(hipEventRecord(c->ev[10], s));
+        HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, ntiles - 1, c->fm,
+                                 c->records.as<uint64_t>(), rec_cap, c->sig_status.as<uint64_t>(),
+                                 c->counters.as<unsigned long long>(), s));
+        HIP_TRY(hipEventRecord(c->ev[11], s));
+        HIP_TRY(hipEventRecord(c->ev[3], s));
+        uint64_t h[4] = {0, 0, 0, 0};
+        HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h[2]) return FK_OK;  // fallback
+        c->nrec = h[0];
+        c->nkmers = h[1];
+        c->stats.positions = h[3];
+        if (c->nrec <= rec_cap) {
+            *ok = true;
+            break;
+        }
+        rec_cap = c->nrec;
+    }
+    c->stats.ms_parse = 0.0;
+    c->stats.ms_signature = ev_ms(c->ev[2], c->ev[3]);
+    c->stats.ms_encode_kernel = 0.0;
+    c->stats.ms_signature_kernel = ev_ms(c->ev[10], c->ev[11]);
+    return FK_OK;
+}
+
 FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
     const double t_start = now_ms();
     hipStream_t s = c->stream;
     c->ingest_fresh = true;  // a later fk_ingest starts a new input
@@ -587,12 +677,16 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         HIP_TRY(hipEventRecord(c->ev[1], s));
         return FK_OK;
     };
+    bool fused_ok = false;
+    if (c->fused && n && map_fused_supported(c->cfg.k, c->cfg.m, (uint32_t)c->Bc)) FK_TRY(map_fused(c, n, &fused_ok));
+    c->last_map_fused = fused_ok;
+    c->stats.fused_map = fused_ok ? 1 : 0;
     bool parse_scan = c->parse_scan;
-    FK_TRY(run_parse(parse_scan));
+    if (!fused_ok) FK_TRY(run_parse(parse_scan));
 
     // 2. signature + super-k-mer records (retried once if the capacity estimate was short)
     uint64_t rec_cap = std::max<uint64_t>(n / 6, 4096);
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    for (int attempt = 0; attempt < 2 && !fused_ok; ++attempt) {
         FK_TRY(ensure(c->records, rec_cap * c->W * 8));
         rec_cap = c->records.bytes / (c->W * 8);
         HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
@@ -624,15 +718,17 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         if (c->nrec <= rec_cap) break;
         rec_cap = c->nrec;
     }
-    uint64_t npos = 0;
-    HIP_TRY(hipMemcpy(&npos, c->npos_dev.p, 8, hipMemcpyDeviceToHost));
-    c->stats.positions = npos;
+    if (!fused_ok) {
+        uint64_t npos = 0;
+        HIP_TRY(hipMemcpy(&npos, c->npos_dev.p, 8, hipMemcpyDeviceToHost));
+        c->stats.positions = npos;
+        c->stats.ms_parse = ev_ms(c->ev[0], c->ev[1]);
+        c->stats.ms_signature = ev_ms(c->ev[2], c->ev[3]);
+        c->stats.ms_encode_kernel = n ? ev_ms(c->ev[8], c->ev[9]) : 0.0;
+        c->stats.ms_signature_kernel = ev_ms(c->ev[10], c->ev[11]);
+    }
     c->stats.kmers = c->nkmers;
     c->stats.superkmers = c->nrec;
-    c->stats.ms_parse = ev_ms(c->ev[0], c->ev[1]);
-    c->stats.ms_signature = ev_ms(c->ev[2], c->ev[3]);
-    c->stats.ms_encode_kernel = n ? ev_ms(c->ev[8], c->ev[9]) : 0.0;
-    c->stats.ms_signature_kernel = ev_ms(c->ev[10], c->ev[11]);
 
     // 3a. destination histogram (records per rank)
     c->send_counts.assign(c->G, 0);
@@ -666,6 +762,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
 
 FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
     if (!c->mapped) return set_err(FK_E_STATE, "fk_map_emit before fk_map");
     if (cap_records < c->nrec) return set_err(FK_E_RANGE, "send buffer holds %llu records, need %llu",
                                               (unsigned long long)cap_records, (unsigned long long)c->nrec);
@@ -691,6 +788,7 @@ FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
 
 FK_EXPORT int fk_map_bin_kmers(fk_ctx *c, uint64_t *kmers_per_bin) {
     if (!c || !kmers_per_bin) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
     if (!c->mapped) return set_err(FK_E_STATE, "fk_map_bin_kmers before fk_map");
     hipStream_t s = c->stream;
     FK_TRY(part_count(c->binhist, c->W, c->records.as<uint64_t>(), c->nrec, 1, 1, nullptr, (uint32_t)c->Bc, c->ws, s));
@@ -724,6 +822,8 @@ FK_EXPORT int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks
 
 FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_counts) {
     if (!c || !owner) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
+    if (c->grouped) return set_err(FK_E_STATE, "size-aware placement with grouped emit enabled (disable it first)");
     for (int32_t b = 0; b < c->Bc; ++b)
         if (owner[b] < 0 || (uint32_t)owner[b] >= c->G)
             return set_err(FK_E_INVALID, "owner[%d] = %d is not a rank of %u", b, owner[b], c->G);
@@ -782,6 +882,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
                                            : (c->KW == 2 && tiered ? WAVE128_BUCKET_CAP / 2 : two_level ? cap / 8 : cap / 4);
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
+    if (!two_level) F = std::min(F, MAX_FINE_BITS - 1);  // one-level scatter: 8 << F bytes of LDS <= 128 KB
     F = std::min(F, 2 * k);
     const uint32_t ncell = 1u << F;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
@@ -1047,6 +1148,7 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
 
 FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
     if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
     const double t0 = now_ms();
     hipStream_t s = c->stream;
@@ -1083,6 +1185,7 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
 
 FK_EXPORT int fk_set_grouped_emit(fk_ctx *c, int32_t enable) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
     if (enable && c->custom_owners)
         return set_err(FK_E_STATE, "grouped emit needs the default placement (bin %% n_ranks)");
     c->grouped = enable != 0;
@@ -1109,6 +1212,7 @@ FK_EXPORT int fk_map_part_counts(fk_ctx *c, uint64_t *records, uint64_t *kmers) 
 FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, const uint64_t *seg_records,
                                 const uint64_t *seg_kmers, int32_t nseg, int32_t parts_per_seg) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
     if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
     if (nseg < 0 || parts_per_seg < 0 || (nseg && (!seg_records || !seg_kmers)))
         return set_err(FK_E_INVALID, "bad segment table");
@@ -1179,6 +1283,7 @@ FK_EXPORT int fk_bin_sizes(fk_ctx *c, uint64_t *out) {
 
 FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *counts, size_t cap, size_t *n) {
     if (!c || !n) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
     if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
     if (bin < 0 || bin >= c->Bc) return set_err(FK_E_RANGE, "bin %d out of [0, %d)", bin, c->Bc);
     if (!owns(c, bin)) {
@@ -1217,6 +1322,7 @@ static int mkdir_p(const std::string &path) {
 // device (fk_format.inc), copied to the host once and written one file per bin.
 FK_EXPORT int fk_write_bins(fk_ctx *c, const char *out_dir) {
     if (!c || !out_dir) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
     if (!c->have_result) return set_err(FK_E_STATE, "no result: call fk_finish or fk_reduce first");
     if (mkdir_p(out_dir) != 0) return set_err(FK_E_IO, "cannot create %s: %s", out_dir, strerror(errno));
     hipStream_t s = c->stream;

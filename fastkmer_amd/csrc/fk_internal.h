@@ -63,6 +63,17 @@ hipError_t launch_superkmers(int W, const uint32_t *codes, const uint32_t *valid
                              uint64_t *status, uint64_t *tile_kmers, unsigned long long *counters, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, uint64_t n, uint64_t v, hipStream_t s);
 
+// ---- fused parse + signature (fk_map_fused.inc): FASTA bytes -> records in one kernel
+// for (k, m) with an instantiation and b <= 8192; tiles of fm_tile_bytes(nth) FASTA bytes
+// (nth = 256 or 512 threads), status[] = look-back words (zeroed), counters[4] =
+// records (set by last_tile), k-mers, fallback flag, positions.
+bool map_fused_supported(int k, int m, uint32_t nbins);
+uint64_t fm_tile_bytes(int nth);
+uint64_t fm_span_bytes(int nth);
+hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
+                            uint64_t ntiles, uint64_t last_tile, FastMod fm, uint64_t *records, uint64_t rec_cap,
+                            uint64_t *status, unsigned long long *counters, hipStream_t s);
+
 // ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]
 // record partition by part = bin % G (mode 0) or bin / G (mode 1).  H, K:
 // nparts * part_workgroups(nrec) u32 each; Hs, Ks: their exclusive scans

@@ -331,6 +331,7 @@ hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWo
 
 #include "fk_parse.inc"
 #include "fk_signature.inc"
+#include "fk_map_fused.inc"
 #include "fk_records.inc"
 #include "fk_partition.inc"
 #include "fk_radix_rank.inc"

@@ -78,8 +78,18 @@ def count_distributed(counter, group=None, device=None, balance: bool = False):
     send = torch.empty(max(total, 1) * rb, dtype=torch.uint8, device=dev)
     counter.map_emit(send.data_ptr(), max(total, 1))
     send = send[: total * rb]
+    host = dist.get_backend(group) == "gloo"
+    ev = None if host else (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if ev:
+        ev[0].record()
     recv, recv_counts = exchange_records(send, send_counts, rb, group)
+    if ev:
+        ev[1].record()
     torch.cuda.synchronize(dev)
+    rank = dist.get_rank(group)
+    counter.last_exchange = {"rounds": 1, "bytes_sent": [(total - send_counts[rank]) * rb],
+                             "bytes_received": [(sum(recv_counts) - recv_counts[rank]) * rb],
+                             "a2a_ms": [ev[0].elapsed_time(ev[1]) if ev else None]}
     counter.reduce(recv.data_ptr(), sum(recv_counts))
     return sum(recv_counts)
 
@@ -192,7 +202,12 @@ def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
     dist.all_to_all_single(rcv, sc, group=group)
     rt = rcv.cpu().numpy().reshape(world, R, 2, parts)  # [source][round][records | k-mers][local bin]
     recv_counts = [[int(rt[src, r, 0].sum()) for src in range(world)] for r in range(R)]  # [round][source]
+    me = dist.get_rank(group)
     works, recvs, off = [], [], 0
+    t_post = None if host else torch.cuda.Event(enable_timing=True)
+    if t_post is not None:
+        t_post.record()
+    sent, received = [], []
     for r in range(R):
         ins = [send_counts[r * world + d] * rb for d in range(world)]
         outs = [c * rb for c in recv_counts[r]]
@@ -200,15 +215,24 @@ def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
         works.append(dist.all_to_all_single(recv, payload[off:off + sum(ins)], output_split_sizes=outs,
                                             input_split_sizes=ins, group=group, async_op=True))
         recvs.append(recv)
+        sent.append(sum(ins) - ins[me])
+        received.append(sum(outs) - outs[me])
         off += sum(ins)
-    n = 0
+    n, done = 0, []
     for r in range(R):
-        works[r].wait()
+        works[r].wait()  # nccl: the current stream waits for round r (the host does not block)
         recv = recvs[r].to(dev) if host else recvs[r]
         if not host:
-            torch.cuda.current_stream(dev).synchronize()  # round r's records have landed
+            # round r's records have landed once the current stream reaches this
+            # event; the count stream waits on it on the device, not the host
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            rc._stream.wait_event(ev)
+            done.append(ev)
         rc.parts[r].reduce_grouped(recv.data_ptr(), sum(recv_counts[r]), rt[:, r, 0, :], rt[:, r, 1, :])
         n += sum(recv_counts[r])
+    rc.last_exchange = {"rounds": R, "bytes_sent": sent, "bytes_received": received,
+                        "a2a_ms": [t_post.elapsed_time(e) for e in done] if done else [None] * R}
     return n
 
 

@@ -69,7 +69,8 @@ typedef struct fk_stats {
     double ms_count;           /* expand + bucket + sort/hash + compact kernels */
     double ms_total;           /* fk_map + fk_reduce wall time on the host */
     double ms_encode_kernel;   /* last launch of the encode kernel */
-    double ms_signature_kernel;/* last launch of the signature kernel */
+    double ms_signature_kernel;/* last launch of the signature kernel (the fused parse + signature kernel when fused_map) */
+    uint64_t fused_map;        /* 1: the last fk_map ran the fused kernel (k_map_fused), 0: parse + signature kernels */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

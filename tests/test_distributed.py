@@ -33,10 +33,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _init(rank: int, world: int, port: int) -> None:
+def _init(rank: int, world: int, port: int, backend: str = "gloo") -> None:
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL over xGMI: one GPU per rank
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
 def _long_fasta(n_blocks=8, seed=5) -> bytes:
@@ -146,12 +150,13 @@ def test_exchange_records_gloo(world, rb):
 
 # ---------------------------------------------------------------- whole job (GPU)
 
-def _job_worker(rank, world, port, cfg_kw, rounds=None):
-    _init(rank, world, port)
+def _job_worker(rank, world, port, cfg_kw, rounds=None, backend="gloo"):
+    _init(rank, world, port, backend)
     try:
         from fastkmer_amd.exchange import execute_job_distributed
-        torch.cuda.set_device(0)
-        kc = execute_job_distributed(fk.TestConfiguration(**cfg_kw), device=torch.device("cuda", 0), rounds=rounds)
+        gpu = rank if backend == "nccl" else 0
+        torch.cuda.set_device(gpu)
+        kc = execute_job_distributed(fk.TestConfiguration(**cfg_kw), device=torch.device("cuda", gpu), rounds=rounds)
         sizes = kc.bin_sizes()
         if not cfg_kw.get("useCustomPartitioner"):
             assert all(sizes[b] == 0 for b in range(kc.num_bins) if b % world != rank)
@@ -190,5 +195,31 @@ def test_execute_job_distributed_two_ranks(tmp_path, use_ht, seq_type, custom, r
             g = got[name].split(b"\n")
             w = want[name].split(b"\n")
             assert sorted(x for x in g if x) == sorted(x for x in w if x)
+        else:
+            assert got[name] == want[name]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL all-to-all needs two GPUs")
+@pytest.mark.parametrize("use_ht,rounds", [(False, 1), (False, 2), (True, None)])
+def test_execute_job_distributed_rccl(tmp_path, use_ht, rounds):
+    """The RCCL transport (torch.distributed "nccl" = RCCL over xGMI): device
+    tensors all the way, one GPU per rank; bin files byte-compared with the
+    oracle's (the reduceByKey shuffle of SBKC:1034-1042)."""
+    k, m, B = 28, 10, 2048
+    data = fk.synth_fasta(40_000, 100, 400_000, seed=23)
+    path = tmp_path / "in.fa"
+    path.write_bytes(data)
+    cfg = dict(dataset=str(path), outputDirectory=str(tmp_path / "out") + "/", k=k, m=m, x=3, max_b=B,
+               sequenceType=0, useHT=use_ht, write=True)
+    mp.spawn(_job_worker, args=(2, _free_port(), cfg, rounds, "nccl"), nprocs=2, join=True)
+    got = _read_bins(fk.TestConfiguration(**cfg).outputDir)
+    ref_dir = tmp_path / "ref"
+    oracle.OracleResult(data, k, m, B).write_bins(str(ref_dir), sorted_eof=not use_ht)
+    want = _read_bins(str(ref_dir))
+    assert sorted(got) == sorted(want)
+    for name in want:
+        if use_ht:
+            assert sorted(x for x in got[name].split(b"\n") if x) == sorted(x for x in want[name].split(b"\n") if x)
         else:
             assert got[name] == want[name]
