@@ -51,7 +51,8 @@ class fk_stats(ctypes.Structure):
                  "oversize_buckets", "buckets", "fine_bits")] + \
                [(n, ctypes.c_double) for n in
                 ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
-                 "ms_signature_kernel")] + [("fused_map", ctypes.c_uint64)]
+                 "ms_signature_kernel")] + [("fused_map", ctypes.c_uint64), ("ms_h2d", ctypes.c_double),
+                                       ("fused_fallback", ctypes.c_uint64)]
 
 
 _lib = None
@@ -98,7 +99,9 @@ def lib():
         "fk_set_stream": (ctypes.c_int, [P, P]),
         "fk_ingest": (ctypes.c_int, [P, ctypes.c_char_p, SZ, ctypes.c_int]),
         "fk_ingest_device": (ctypes.c_int, [P, P, SZ, ctypes.c_int]),
+        "fk_ingest_reserve": (ctypes.c_int, [P, U64]),
         "fk_synth_fasta_device": (ctypes.c_int, [P, U64, U64, I32, U64, U64, ctypes.c_double, ctypes.c_double]),
+        "fk_synth_fasta_to_device": (ctypes.c_int, [P, U64, U64, I32, U64, U64, ctypes.c_double, ctypes.c_double]),
         "fk_map": (ctypes.c_int, [P, P]),
         "fk_record_bytes": (SZ, [P]),
         "fk_map_emit": (ctypes.c_int, [P, P, U64]),
@@ -162,6 +165,16 @@ def synth_fasta(n_reads: int, read_len: int = 100, genome_len: int = 1_000_000, 
     buf = ctypes.create_string_buffer(max(nb, 1))
     _check(L.fk_synth_fasta_host(buf, first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate))
     return buf.raw[:nb]
+
+
+def synth_fasta_to_device(ptr: int, n_reads: int, read_len: int = 100, genome_len: int = 1_000_000,
+                          seed: int = 0x5EED, err_rate: float = 0.002, n_rate: float = 0.0005,
+                          first_read: int = 0) -> int:
+    """The bytes of synth_fasta written into a device buffer at ptr (current device); returns the size."""
+    L = lib()
+    _check(L.fk_synth_fasta_to_device(ctypes.c_void_p(ptr), first_read, n_reads, read_len, genome_len, seed,
+                                      err_rate, n_rate))
+    return n_reads * L.fk_synth_record_bytes(read_len)
 
 
 def decode_keys(keys: np.ndarray, k: int) -> list[str]:
@@ -249,9 +262,17 @@ class KmerCounter:
         self._keep = bytes(fasta)
         _check(lib().fk_ingest(self._h, self._keep, len(self._keep), 1))
 
-    def ingest_ptr(self, ptr: int, n: int) -> None:
+    def ingest_ptr(self, ptr: int, n: int, last: bool = True) -> None:
         """Append n host bytes at ptr (pinned memory is copied by DMA directly)."""
-        _check(lib().fk_ingest(self._h, ctypes.cast(ptr, ctypes.c_char_p), n, 1))
+        _check(lib().fk_ingest(self._h, ctypes.cast(ptr, ctypes.c_char_p), n, 1 if last else 0))
+
+    def ingest_chunk(self, chunk: bytes, last: bool) -> None:
+        """Streamed input: append one chunk (the map of the landed bytes overlaps the copies)."""
+        _check(lib().fk_ingest(self._h, chunk, len(chunk), 1 if last else 0))
+
+    def reserve(self, total_bytes: int) -> None:
+        """Size the device input for a streamed ingest of about total_bytes."""
+        _check(lib().fk_ingest_reserve(self._h, total_bytes))
 
     def ingest_device(self, ptr: int, n: int) -> None:
         _check(lib().fk_ingest_device(self._h, ctypes.c_void_p(ptr), n, 1))

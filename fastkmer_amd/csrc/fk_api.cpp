@@ -227,6 +227,15 @@ struct fk_ctx {
     bool ingest_fresh = true;        // the next fk_ingest starts a new input
     void *pinned[2] = {nullptr, nullptr};  // staging for pageable sources
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;     // H2D of fk_ingest (the map runs on `stream` meanwhile)
+    hipEvent_t seg_ev = nullptr;           // "segment landed" (copy stream -> map stream)
+    hipEvent_t h2d_ev[2] = {nullptr, nullptr};  // first copy issued / last copy done (timing)
+    // streamed map (fused path): fk_ingest maps every tile whose bytes (and halo) have landed
+    bool pm_active = false;     // the current input is being mapped while it is copied
+    uint64_t pm_tiles = 0;      // tiles [0, pm_tiles) launched
+    uint64_t pm_rec_cap = 0;    // smallest record capacity any launch used
+    uint64_t pm_status_tiles = 0;  // look-back words allocated and zeroed
+    bool pm_last_seen = false;  // an fk_ingest with last = 1 launched the final tiles
     const uint8_t *d_fasta = nullptr;
     uint64_t n_fasta = 0;
     DevBuf fasta_own;
@@ -254,6 +263,7 @@ struct fk_ctx {
     fk_stats stats{};
     // events: 0/1 parse, 2/3 signature, 4/5 partition, 6/7 count, 8/9 encode kernel, 10/11 sig kernel
     hipEvent_t ev[12] = {};
+    double ms_h2d = 0.0;  // last fk_ingest: first copy issued -> last copy done
     bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
 };
 
@@ -414,6 +424,13 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         return set_err(FK_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->own_stream = true;
+    e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->seg_ev, hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreate(&c->h2d_ev[i]);
+    if (e != hipSuccess) {
+        fk_destroy(c);
+        return set_err(FK_E_DEVICE, "copy stream / events: %s", hipGetErrorString(e));
+    }
     for (auto &ev : c->ev) {
         e = hipEventCreate(&ev);
         if (e != hipSuccess) {
@@ -428,6 +445,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (!c) return;
     DeviceGuard dg_(c->device);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
@@ -450,6 +468,10 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->ws.ptr) (void)hipFree(c->ws.ptr);
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (c->seg_ev) (void)hipEventDestroy(c->seg_ev);
+    for (auto &ev : c->h2d_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -476,14 +498,61 @@ static void reset_results(fk_ctx *c) {
     c->h_bin_off.clear();
 }
 
-constexpr size_t PIN_CHUNK = 64ull << 20;  // pinned staging buffer (x2) for pageable sources
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0.f;
+    }
+    return ms;
+}
 
-// Appends host bytes to the device input.  Pinned sources are copied by DMA
-// directly; pageable ones through two pinned staging buffers, the memcpy of
-// one chunk overlapping the DMA of the previous one.  Returns after the
-// source has been read.
+constexpr size_t PIN_CHUNK = 32ull << 20;  // pinned staging buffer (x2) for pageable sources
+constexpr size_t INGEST_SEG = 32ull << 20;  // H2D segment: the tiles it completes are mapped while the next lands
+
+// Grows b to at least `bytes`, keeping its first `keep` bytes (stream-ordered copy).
+static int grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s) {
+    if (b.bytes >= bytes) return FK_OK;
+    DevBuf g;
+    FK_TRY(ensure(g, std::max<size_t>(bytes, 2 * b.bytes)));
+    if (keep && b.p) HIP_TRY(hipMemcpyAsync(g.p, b.p, std::min(keep, b.bytes), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    release(b);
+    b = g;
+    return FK_OK;
+}
+
+static bool premap_eligible(const fk_ctx *c) {
+    return c->fused && map_fused_supported(c->cfg.k, c->cfg.m, (uint32_t)c->Bc);
+}
+
+// Streamed map: launches the fused map over the tiles whose bytes (and halo)
+// lie below `landed`; `final_` = the input ends at `landed` (every remaining
+// tile, the last one sets the record total).  Runs on the map stream after
+// the copy stream's segment event.
+static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
+    const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
+    const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
+    if (end <= c->pm_tiles) return FK_OK;
+    hipStream_t s = c->stream;
+    if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
+    HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
+                             end - c->pm_tiles, final_ ? end - 1 : ~0ull, c->fm, c->records.as<uint64_t>(),
+                             c->pm_rec_cap, c->sig_status.as<uint64_t>(), c->counters.as<unsigned long long>(), s));
+    c->pm_tiles = end;
+    if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
+    return FK_OK;
+}
+
+// Appends host bytes to the device input on the copy stream, in segments.
+// Pinned sources are copied by DMA directly; pageable ones through two
+// pinned staging buffers (the memcpy of one overlapping the DMA of the
+// other).  With the fused map (k_map_fused) every tile whose bytes have
+// landed is mapped on the map stream while the next segment is in flight,
+// so the PCIe transfer hides the parse + signature work.  Returns once the
+// source has been read (the caller's buffer is free); the map of the last
+// segment may still be running.
 FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
-    (void)last;
     if (!c || (!fasta && n)) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
     if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>()) {
@@ -492,47 +561,95 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         if (!c->ingest_fresh) return set_err(FK_E_STATE, "fk_ingest appending to an fk_ingest_device input");
         c->d_fasta = nullptr;
     }
-    hipStream_t s = c->stream;
-    if (c->ingest_fresh || !c->d_fasta) {
+    hipStream_t s = c->stream, cs = c->copy_stream;
+    const bool fresh = c->ingest_fresh || !c->d_fasta;
+    if (fresh) {
         c->n_fasta = 0;
         c->ingest_fresh = false;
+        HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
+        c->pm_active = premap_eligible(c);
+        c->pm_tiles = 0;
+        c->pm_status_tiles = 0;
+        c->pm_rec_cap = ~0ull;
+        c->pm_last_seen = false;
+    } else if (c->pm_last_seen) {
+        c->pm_active = false;  // appending after the final tiles: fk_map maps the whole input
     }
     const uint64_t have = c->n_fasta, need = have + n;
-    if (c->fasta_own.bytes < need) {  // grow, keeping what was ingested
-        DevBuf grown;
-        FK_TRY(ensure(grown, std::max<uint64_t>(need, 2 * (uint64_t)c->fasta_own.bytes)));
-        if (have) HIP_TRY(hipMemcpyAsync(grown.p, c->fasta_own.p, have, hipMemcpyDeviceToDevice, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        release(c->fasta_own);
-        c->fasta_own = grown;
+    if (c->fasta_own.bytes < need) {  // grow, keeping what was ingested (and what the map reads)
+        HIP_TRY(hipStreamSynchronize(cs));
+        FK_TRY(grow_keep(c->fasta_own, need, have, s));
+    }
+    c->d_fasta = c->fasta_own.as<uint8_t>();
+    if (c->pm_active) {
+        const uint64_t tiles = (need + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
+        if (c->pm_status_tiles < tiles) {  // look-back words: kept, the new ones zeroed
+            const uint64_t want = std::max<uint64_t>(tiles, 2 * c->pm_status_tiles);
+            FK_TRY(grow_keep(c->sig_status, want * 8, c->pm_status_tiles * 8, s));
+            HIP_TRY(hipMemsetAsync(c->sig_status.as<uint64_t>() + c->pm_status_tiles, 0,
+                                   (want - c->pm_status_tiles) * 8, s));
+            c->pm_status_tiles = want;
+        }
+        if (fresh) {
+            FK_TRY(ensure(c->counters, 64));
+            HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
+        }
+        const uint64_t cap_need = std::max<uint64_t>(need / 6, 4096);
+        if (c->records.bytes < cap_need * c->W * 8) {
+            // records of the tiles mapped so far are kept; a launch that ran with
+            // a smaller capacity is caught by fk_map through pm_rec_cap
+            FK_TRY(grow_keep(c->records, cap_need * c->W * 8, c->records.bytes, s));
+        }
+        c->pm_rec_cap = std::min<uint64_t>(c->pm_rec_cap, c->records.bytes / (c->W * 8));
     }
     uint8_t *dst = c->fasta_own.as<uint8_t>() + have;
     hipPointerAttribute_t attr{};
     const bool pinned = hipPointerGetAttributes(&attr, fasta) == hipSuccess && attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();
-    if (pinned || n == 0) {
-        if (n) HIP_TRY(hipMemcpyAsync(dst, fasta, n, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipStreamSynchronize(s));
-    } else {
+    if (!pinned && n)
         for (int i = 0; i < 2; ++i)
             if (!c->pinned[i]) {
                 HIP_TRY(hipHostMalloc(&c->pinned[i], PIN_CHUNK, hipHostMallocDefault));
                 HIP_TRY(hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(c->pin_ev[i], s));
+                HIP_TRY(hipEventRecord(c->pin_ev[i], cs));
             }
-        size_t off = 0;
-        for (int i = 0; off < n; ++i) {
-            const size_t len = std::min(PIN_CHUNK, n - off);
+    HIP_TRY(hipEventRecord(c->h2d_ev[0], cs));
+    size_t off = 0;
+    for (int i = 0; off < n; ++i) {
+        const size_t len = std::min(pinned ? INGEST_SEG : PIN_CHUNK, n - off);
+        if (pinned) {
+            HIP_TRY(hipMemcpyAsync(dst + off, fasta + off, len, hipMemcpyHostToDevice, cs));
+        } else {
             HIP_TRY(hipEventSynchronize(c->pin_ev[i & 1]));  // its previous DMA is done
             memcpy(c->pinned[i & 1], fasta + off, len);
-            HIP_TRY(hipMemcpyAsync(dst + off, c->pinned[i & 1], len, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipEventRecord(c->pin_ev[i & 1], s));
-            off += len;
+            HIP_TRY(hipMemcpyAsync(dst + off, c->pinned[i & 1], len, hipMemcpyHostToDevice, cs));
+            HIP_TRY(hipEventRecord(c->pin_ev[i & 1], cs));
+        }
+        off += len;
+        if (c->pm_active) {
+            HIP_TRY(hipEventRecord(c->seg_ev, cs));
+            HIP_TRY(hipStreamWaitEvent(s, c->seg_ev, 0));
+            FK_TRY(premap_launch(c, have + off, last && off == n));
         }
     }
-    c->d_fasta = c->fasta_own.as<uint8_t>();
+    HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
+    if (c->pm_active && last) {
+        c->pm_last_seen = true;
+        if (n == 0) FK_TRY(premap_launch(c, need, true));
+    }
+    HIP_TRY(hipStreamSynchronize(cs));  // the source has been read
+    c->ms_h2d = ev_ms(c->h2d_ev[0], c->h2d_ev[1]);
     c->n_fasta = need;
     reset_results(c);
+    return FK_OK;
+}
+
+FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
+    if (!c->ingest_fresh && c->d_fasta) return set_err(FK_E_STATE, "fk_ingest_reserve inside a streamed input");
+    FK_TRY(ensure(c->fasta_own, total_bytes));
+    if (premap_eligible(c)) FK_TRY(ensure(c->records, std::max<uint64_t>(total_bytes / 6, 4096) * c->W * 8));
     return FK_OK;
 }
 
@@ -541,6 +658,7 @@ FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
     if (!c || (!d && n)) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
     c->ingest_fresh = true;
+    c->pm_active = false;
     reset_results(c);
     if (((uintptr_t)d & 15) != 0) {
         FK_TRY(ensure(c->fasta_own, n));
@@ -550,6 +668,16 @@ FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
         c->d_fasta = (const uint8_t *)d;
     }
     c->n_fasta = n;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_synth_fasta_to_device(void *d_out, uint64_t first_read, uint64_t n_reads, int32_t read_len,
+                                       uint64_t genome_len, uint64_t seed, double err_rate, double n_rate) {
+    if ((!d_out && n_reads) || read_len < 1 || genome_len < 1) return set_err(FK_E_INVALID, "bad synth arguments");
+    const SynthParams p = make_synth(first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate);
+    const uint64_t nb = n_reads * p.rec_bytes;
+    if (nb) HIP_TRY(launch_synth((uint8_t *)d_out, nb, p, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
     return FK_OK;
 }
 
@@ -563,6 +691,7 @@ FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_r
     HIP_TRY(launch_synth(c->fasta_own.as<uint8_t>(), nb, p, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->ingest_fresh = true;
+    c->pm_active = false;
     c->d_fasta = c->fasta_own.as<uint8_t>();
     c->n_fasta = nb;
     reset_results(c);
@@ -573,14 +702,6 @@ FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_r
 // map side: parse + encode + signature + records (+ destination histogram)
 // ---------------------------------------------------------------------------
 
-static float ev_ms(hipEvent_t a, hipEvent_t b) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
-        (void)hipGetLastError();
-        return 0.f;
-    }
-    return ms;
-}
 
 static const uint32_t *owner_table(const fk_ctx *c) { return c->custom_owners ? c->d_owner.as<uint32_t>() : nullptr; }
 static const uint32_t *local_table(const fk_ctx *c) { return c->custom_owners ? c->d_local.as<uint32_t>() : nullptr; }
@@ -614,6 +735,7 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
         uint64_t h[4] = {0, 0, 0, 0};
         HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        c->stats.fused_fallback = h[2];
         if (h[2]) return FK_OK;  // fallback
         c->nrec = h[0];
         c->nkmers = h[1];
@@ -643,18 +765,49 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     c->stats.fasta_bytes = n;
     c->nrec = c->nkmers = 0;
 
+    // 0. fused parse + signature (streamed by fk_ingest, or one launch here); the
+    // two-kernel path below maps the inputs the fused kernel hands back
+    bool fused_ok = false;
+    c->stats.ms_h2d = c->ms_h2d;
+    if (c->pm_active && n) {
+        // streamed map (fk_ingest launched the tiles as their bytes landed)
+        if (!c->pm_last_seen) FK_TRY(premap_launch(c, n, true));  // the input ends here
+        uint64_t h[4] = {0, 0, 0, 0};
+        HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->stats.fused_fallback = h[2];
+        if (!h[2] && h[0] <= c->pm_rec_cap) {
+            fused_ok = true;
+            c->nrec = h[0];
+            c->nkmers = h[1];
+            c->stats.positions = h[3];
+            c->stats.ms_parse = 0.0;
+            // map stream from the first to the last launch, waits for the landing segments included
+            c->stats.ms_signature = ev_ms(c->ev[10], c->ev[11]);
+            c->stats.ms_signature_kernel = c->stats.ms_signature;
+        } else if (!h[2]) {
+            FK_TRY(map_fused(c, n, &fused_ok));  // record capacity: remap the resident input at once
+        }
+        c->pm_active = false;
+    } else if (c->fused && n && map_fused_supported(c->cfg.k, c->cfg.m, (uint32_t)c->Bc)) {
+        FK_TRY(map_fused(c, n, &fused_ok));
+    }
+    c->pm_active = false;
+
     const uint64_t ntiles = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t code_words = n / 16 + 2 * POS_PAD_WORDS + 512;
     const uint64_t valid_words = n / 32 + 2 * POS_PAD_WORDS + 512;
-    FK_TRY(ensure(c->tile_last_nl, ntiles * 8));  // look-back status: newline / header state
-    FK_TRY(ensure(c->tile_off, ntiles * 8));      // look-back status: output positions
-    FK_TRY(ensure(c->npos_dev, 16));  // [0] positions, [1] "rerun the parse with the look-back"
-    FK_TRY(ensure(c->codes, code_words * 4));
-    FK_TRY(ensure(c->valid, valid_words * 4));
-    FK_TRY(ensure(c->counters, 64));
     const uint64_t sig_tiles = (n + SIG_TILE - 1) / SIG_TILE + 1;
-    FK_TRY(ensure(c->sig_status, sig_tiles * 8));
-    FK_TRY(ensure(c->sig_kmers, sig_tiles * 8));
+    if (!fused_ok) {
+        FK_TRY(ensure(c->tile_last_nl, ntiles * 8));  // look-back status: newline / header state
+        FK_TRY(ensure(c->tile_off, ntiles * 8));      // look-back status: output positions
+        FK_TRY(ensure(c->npos_dev, 16));  // [0] positions, [1] "rerun the parse with the look-back"
+        FK_TRY(ensure(c->codes, code_words * 4));
+        FK_TRY(ensure(c->valid, valid_words * 4));
+        FK_TRY(ensure(c->counters, 64));
+        FK_TRY(ensure(c->sig_status, sig_tiles * 8));
+        FK_TRY(ensure(c->sig_kmers, sig_tiles * 8));
+    }
 
     // 1. FASTA parse + 2-bit encode.  The scan variant flags inputs it cannot
     // place (a line longer than its read-back, text before the first header);
@@ -677,8 +830,6 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         HIP_TRY(hipEventRecord(c->ev[1], s));
         return FK_OK;
     };
-    bool fused_ok = false;
-    if (c->fused && n && map_fused_supported(c->cfg.k, c->cfg.m, (uint32_t)c->Bc)) FK_TRY(map_fused(c, n, &fused_ok));
     c->last_map_fused = fused_ok;
     c->stats.fused_map = fused_ok ? 1 : 0;
     bool parse_scan = c->parse_scan;

@@ -71,6 +71,9 @@ typedef struct fk_stats {
     double ms_encode_kernel;   /* last launch of the encode kernel */
     double ms_signature_kernel;/* last launch of the signature kernel (the fused parse + signature kernel when fused_map) */
     uint64_t fused_map;        /* 1: the last fk_map ran the fused kernel (k_map_fused), 0: parse + signature kernels */
+    double ms_h2d;             /* last fk_ingest: host-to-device copy, first segment issued to last landed */
+    uint64_t fused_fallback;   /* why the fused kernel handed the input back: 1 long line, 2 text before the
+                                  first header, 4 halo too short, 8 too many records in a tile (0: none) */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
@@ -101,10 +104,22 @@ const char *fk_last_error(void);
 int fk_set_stream(fk_ctx *ctx, void *hip_stream);
 
 /* Input.  fk_ingest copies host FASTA bytes to the device (may be called
- * repeatedly: the chunks are concatenated).  fk_ingest_device borrows a
- * device buffer (zero-copy; it must stay valid until fk_map returns). */
+ * repeatedly: the chunks are concatenated; last = 1 marks the final chunk).
+ * The copy runs in segments on the context's copy stream and, for the fused
+ * map configurations, every tile whose bytes have landed is mapped while the
+ * next segment is in flight; the call returns once the source has been read.
+ * fk_ingest_device borrows a device buffer (zero-copy; it must stay valid
+ * until fk_map returns, and one borrowed input is mapped once). */
 int fk_ingest(fk_ctx *ctx, const uint8_t *fasta, size_t n, int last);
+/* Optional, before a streamed fk_ingest sequence: size the device input for
+ * about total_bytes, so the copies of later chunks overlap the map without a
+ * reallocation (FASTdoop-style streaming ingest). */
+int fk_ingest_reserve(fk_ctx *ctx, uint64_t total_bytes);
 int fk_ingest_device(fk_ctx *ctx, const void *d_fasta, size_t n, int last);
+/* Fill a caller's device buffer (current device) with the same bytes as
+ * fk_synth_fasta_host (benchmarks: the input is staged to pinned host memory). */
+int fk_synth_fasta_to_device(void *d_out, uint64_t first_read, uint64_t n_reads, int32_t read_len,
+                             uint64_t genome_len, uint64_t seed, double err_rate, double n_rate);
 /* Fill the device input with fk_synth_fasta-compatible data (benchmarks). */
 int fk_synth_fasta_device(fk_ctx *ctx, uint64_t first_read, uint64_t n_reads, int32_t read_len,
                           uint64_t genome_len, uint64_t seed, double err_rate, double n_rate);

@@ -59,7 +59,7 @@ def test_fused_random_vs_oracle(monkeypatch, nt, k, m, x, B, seed):
     fasta = _fasta(rng, 3000, 1, 400, noise=0.01)
     kc = _run(fasta, k, m, x, B, nt=nt, monkeypatch=monkeypatch)
     st = kc.stats()
-    assert st["fused_map"] == 1, "the fused kernel should place this input"
+    assert st["fused_map"] == 1, ("the fused kernel should place this input", st["fused_fallback"])
     ref = oracle.OracleResult(fasta, k, m, B)
     assert st["kmers"] == ref.total_kmers
     assert_same_as_oracle(kc, ref)
@@ -92,7 +92,8 @@ def test_fused_matches_two_kernel_path_records(monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["long_header", "long_line", "junk_first", "one_base_lines", "crlf",
-                                  "header_across_tiles", "tiny", "empty", "no_newline_end", "blank_lines"])
+                                  "header_across_tiles", "header_at_chunk_start", "tiny", "empty",
+                                  "no_newline_end", "blank_lines"])
 @pytest.mark.parametrize("nt", [256, 512])
 def test_fused_edge_inputs_vs_oracle(monkeypatch, case, nt):
     rng = random.Random(sum(case.encode()))
@@ -120,6 +121,12 @@ def test_fused_edge_inputs_vs_oracle(monkeypatch, case, nt):
         fasta = _fasta(rng, 800, 50, 300, crlf=True)
     elif case == "header_across_tiles":  # headers of 100-3000 bytes straddle tile boundaries
         fasta = _fasta(rng, 500, 20, 200, header_len=(100, 3000))
+    elif case == "header_at_chunk_start":
+        # 256-byte records: every header starts right after a newline at the last byte of a thread's
+        # 64-byte chunk and runs through the next chunk (its line state comes from that newline's
+        # thread); the headers are A/C/G/T text, so counting them as sequence would show
+        fasta = b"".join(b">" + "".join(rng.choice("ACGT") for _ in range(148)).encode() + b"\n" +
+                         "".join(rng.choice("ACGT") for _ in range(105)).encode() + b"\n" for _ in range(600))
     elif case == "tiny":
         fasta = b">r\nACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTAC\n"
     elif case == "empty":
@@ -134,7 +141,7 @@ def test_fused_edge_inputs_vs_oracle(monkeypatch, case, nt):
         assert st["kmers"] == ref.total_kmers
         assert_same_as_oracle(kc, ref)
         if case not in ("tiny",):
-            assert st["fused_map"] == (1 if expect_fused else 0), case
+            assert st["fused_map"] == (1 if expect_fused else 0), (case, st["fused_fallback"])
         kc.close()
 
 
@@ -149,7 +156,7 @@ def test_fused_long_sequence_type1_vs_oracle(monkeypatch):
     body = "".join(seq)
     fasta = (">chrT\n" + "\n".join(body[q:q + 60] for q in range(0, len(body), 60)) + "\n").encode()
     kc = _run(fasta, 28, 10, 3, 2048, sequence_type=1)
-    assert kc.stats()["fused_map"] == 1
+    assert kc.stats()["fused_map"] == 1, kc.stats()["fused_fallback"]
     ref = oracle.OracleResult(fasta, 28, 10, 2048, 1)
     assert_same_as_oracle(kc, ref)
 
@@ -173,3 +180,89 @@ def test_fused_full_size_matches_two_kernel_path(monkeypatch):
         ka, ca = a.get_bin(bin_)
         kb, cb = b.get_bin(bin_)
         assert np.array_equal(ka, kb) and np.array_equal(ca, cb)
+
+
+# ---------------------------------------------------------------- streamed ingest (fk_ingest segments)
+
+def _stream(kc, data: bytes, sizes, last_flag=True):
+    off = 0
+    for i, n in enumerate(sizes):
+        chunk = data[off:off + n]
+        off += n
+        kc.ingest_chunk(chunk, last_flag and off >= len(data))
+        if off >= len(data):
+            break
+    if off < len(data):
+        kc.ingest_chunk(data[off:], last_flag)
+
+
+@pytest.mark.parametrize("reserve,last_flag", [(True, True), (False, True), (False, False)])
+def test_streamed_ingest_chunks_vs_oracle(reserve, last_flag):
+    # chunks of random sizes (1 byte .. 300 kB): tiles are mapped as their bytes and halo land,
+    # the input buffer, look-back words and records grow mid-stream without reserve, and without
+    # a final last=1 chunk fk_map launches the remaining tiles
+    rng = random.Random(31)
+    data = _fasta(rng, 6000, 20, 400)
+    sizes = [rng.choice([1, 7, 100, 4096, 30_000, 65_536, 300_000]) for _ in range(400)]
+    for k, m, x, B in CONFIGS:
+        kc = fk.KmerCounter(k, m, x, B)
+        if reserve:
+            kc.reserve(len(data))
+        _stream(kc, data, sizes, last_flag)
+        kc.finish()
+        assert kc.stats()["fused_map"] == 1
+        ref = oracle.OracleResult(data, k, m, B)
+        assert kc.stats()["kmers"] == ref.total_kmers
+        assert_same_as_oracle(kc, ref)
+        # the context is reused for a second job (the previous records are not carried over)
+        _stream(kc, data[: len(data) // 3], [50_000] * 100, True)
+        kc.finish()
+        ref2 = oracle.OracleResult(data[: len(data) // 3], k, m, B)
+        assert_same_as_oracle(kc, ref2)
+        kc.close()
+
+
+def test_streamed_ingest_fallback_vs_oracle():
+    # a long header line straddling tile starts: the streamed fused map raises the fallback
+    # flag and fk_map maps the resident input with the two-kernel path
+    rng = random.Random(32)
+    body = b""
+    while len(body) < 59_500:
+        body += _fasta(rng, 1, 50, 200)
+    data = body + b">" + b"h" * 10_000 + b"\n" + _fasta(rng, 3000, 50, 200)[1:]
+    kc = fk.KmerCounter(28, 10, 3, 2048)
+    _stream(kc, data, [20_000] * 100)
+    kc.finish()
+    assert kc.stats()["fused_map"] == 0
+    assert_same_as_oracle(kc, oracle.OracleResult(data, 28, 10, 2048))
+
+
+def test_streamed_long_record_sequence_type1_vs_oracle():
+    rng = random.Random(33)
+    seq = "".join(rng.choice("ACGT") for _ in range(400_000))
+    seq = seq[:100_000] + "N" * 2000 + seq[102_000:]
+    data = (">chrU\n" + "\n".join(seq[q:q + 60] for q in range(0, len(seq), 60)) + "\n").encode()
+    kc = fk.KmerCounter(28, 10, 3, 2048, sequence_type=1)
+    _stream(kc, data, [33_333] * 100)
+    kc.finish()
+    assert kc.stats()["fused_map"] == 1, kc.stats()["fused_fallback"]
+    assert_same_as_oracle(kc, oracle.OracleResult(data, 28, 10, 2048, 1))
+
+
+def test_pinned_ingest_overlapped_vs_oracle():
+    # 64 MB from pinned host memory: 32 MB DMA segments on the copy stream, the fused map of
+    # each landed segment overlapping the next copy
+    import torch
+    n_reads = 64_000_000 // 114
+    data = fk.synth_fasta(n_reads, 100, 2_000_000, seed=34)
+    pinned = torch.empty(len(data), dtype=torch.uint8).pin_memory()
+    pinned.numpy()[:] = np.frombuffer(data, dtype=np.uint8)
+    kc = fk.KmerCounter(28, 10, 3, 2048)
+    for _ in range(2):  # the second job reuses the context's buffers
+        kc.ingest_ptr(pinned.data_ptr(), len(data))
+        kc.finish()
+        st = kc.stats()
+        assert st["fused_map"] == 1 and st["ms_h2d"] > 0
+    ref = oracle.OracleResult(data, 28, 10, 2048, threads=8)
+    assert st["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref)
