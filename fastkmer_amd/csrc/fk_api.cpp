@@ -211,6 +211,7 @@ struct fk_ctx {
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
+    int fused_probe = 0;       // FASTKMER_FUSED_PROBE: stop the fused map kernel after a phase (timing only)
     int fused_nt = 512;        // FASTKMER_FUSED_NT: threads per fused map workgroup (256 or 512)
     bool last_map_fused = false;  // the last fk_map used the fused kernel (stats, tests)
     // grouped emit (fk_set_grouped_emit): send buffer grouped by (destination, local bin)
@@ -398,6 +399,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (fu && fu[0]) c->fused = atoi(fu);
     const char *fn = getenv("FASTKMER_FUSED_NT");
     if (fn && fn[0]) c->fused_nt = atoi(fn) == 256 ? 256 : 512;
+    const char *fp = getenv("FASTKMER_FUSED_PROBE");
+    if (fp && fp[0]) c->fused_probe = atoi(fp);
     const char *cm = getenv("FASTKMER_COUNT_MODE");
     if (cm && cm[0]) c->count_mode = atoi(cm);
     if (cfg->device >= 0) {
@@ -538,7 +541,8 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
                              end - c->pm_tiles, final_ ? end - 1 : ~0ull, c->fm, c->records.as<uint64_t>(),
-                             c->pm_rec_cap, c->sig_status.as<uint64_t>(), c->counters.as<unsigned long long>(), s));
+                             c->pm_rec_cap, c->sig_status.as<uint64_t>(), c->counters.as<unsigned long long>(), s,
+                             c->fused_probe));
     c->pm_tiles = end;
     if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
     return FK_OK;
@@ -729,7 +733,7 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
         HIP_TRY(hipEventRecord(c->ev[10], s));
         HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, ntiles - 1, c->fm,
                                  c->records.as<uint64_t>(), rec_cap, c->sig_status.as<uint64_t>(),
-                                 c->counters.as<unsigned long long>(), s));
+                                 c->counters.as<unsigned long long>(), s, c->fused_probe));
         HIP_TRY(hipEventRecord(c->ev[11], s));
         HIP_TRY(hipEventRecord(c->ev[3], s));
         uint64_t h[4] = {0, 0, 0, 0};

@@ -72,7 +72,7 @@ uint64_t fm_tile_bytes(int nth);
 uint64_t fm_span_bytes(int nth);
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
                             uint64_t ntiles, uint64_t last_tile, FastMod fm, uint64_t *records, uint64_t rec_cap,
-                            uint64_t *status, unsigned long long *counters, hipStream_t s);
+                            uint64_t *status, unsigned long long *counters, hipStream_t s, int probe = 0);
 
 // ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]
 // record partition by part = bin % G (mode 0) or bin / G (mode 1).  H, K:

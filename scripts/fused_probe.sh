@@ -1,0 +1,8 @@
+#!/bin/bash
+# Fused map kernel stopped after each phase (FASTKMER_FUSED_PROBE): 1 byte classes + line state,
+# 2 compaction, 3 signature passes, 4 look-back, 0 whole kernel.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+for p in 1 2 3 4 0; do
+  echo -n "probe $p: "
+  FASTKMER_FUSED_PROBE=$p FK_MAP_REPS=15 timeout -k 10 120 python3 scripts/map_once.py || exit 1
+done
