@@ -87,7 +87,7 @@ struct PartBufs {
     DevBuf H, K, Hs, Ks;                  // per-workgroup histograms (column-major) and their scans
     DevBuf rec, kmer, off, cursor;        // per-part totals / offsets (device), cursor: global path only
     uint32_t nparts = 0;
-    uint64_t nrec = 0;
+    RecSrc src{};                         // the records counted (part_scatter reads the same)
     bool global = false;                  // nparts > PART_MAX: global-atomic kernels
     void release_all() {
         for (DevBuf *b : {&H, &K, &Hs, &Ks, &rec, &kmer, &off, &cursor}) release(*b);
@@ -96,10 +96,10 @@ struct PartBufs {
 
 // Counts records and k-mers per part into pb.rec / pb.kmer (device) and keeps
 // what part_scatter needs.
-int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mode, uint32_t G, const uint32_t *table,
-               uint32_t nparts, ScanWorkspace &ws, hipStream_t s) {
+int part_count(PartBufs &pb, const RecSrc &src, int mode, uint32_t G, const uint32_t *table, uint32_t nparts,
+               ScanWorkspace &ws, hipStream_t s) {
     pb.nparts = nparts;
-    pb.nrec = nrec;
+    pb.src = src;
     pb.global = nparts > PART_MAX;
     FK_TRY(ensure(pb.rec, ((uint64_t)nparts + 1) * 8));
     FK_TRY(ensure(pb.kmer, ((uint64_t)nparts + 1) * 8));
@@ -107,22 +107,22 @@ int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mod
     if (pb.global) {
         HIP_TRY(hipMemsetAsync(pb.rec.p, 0, ((uint64_t)nparts + 1) * 8, s));
         HIP_TRY(hipMemsetAsync(pb.kmer.p, 0, ((uint64_t)nparts + 1) * 8, s));
-        HIP_TRY(launch_part_hist_global(W, recs, nrec, mode, G, table, nparts, pb.rec.as<uint64_t>(),
-                                        pb.kmer.as<uint64_t>(), s));
+        HIP_TRY(launch_part_hist_global(src, mode, G, table, nparts, pb.rec.as<uint64_t>(), pb.kmer.as<uint64_t>(), s));
         HIP_TRY(scan_excl_sum_u64(pb.rec.as<uint64_t>(), pb.off.as<uint64_t>(), nparts, pb.off.as<uint64_t>() + nparts,
                                   ws, s));
         return FK_OK;
     }
-    const uint64_t n = (uint64_t)nparts * part_workgroups(nrec);
+    const uint32_t nwg = src.nrec ? part_workgroups(src) : 0u;
+    const uint64_t n = (uint64_t)nparts * nwg;
     FK_TRY(ensure(pb.H, n * 4));
     FK_TRY(ensure(pb.K, n * 4));
     FK_TRY(ensure(pb.Hs, (n + 1) * 8));
     FK_TRY(ensure(pb.Ks, (n + 1) * 8));
     if (n) {
-        HIP_TRY(launch_part_hist(W, recs, nrec, mode, G, table, nparts, pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), s));
+        HIP_TRY(launch_part_hist(src, mode, G, table, nparts, pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), s));
         HIP_TRY(scan_excl_sum_u32_to_u64(pb.H.as<uint32_t>(), pb.Hs.as<uint64_t>(), n, pb.Hs.as<uint64_t>() + n, ws, s));
         HIP_TRY(scan_excl_sum_u32_to_u64(pb.K.as<uint32_t>(), pb.Ks.as<uint64_t>(), n, pb.Ks.as<uint64_t>() + n, ws, s));
-        HIP_TRY(launch_part_totals(pb.Hs.as<uint64_t>(), pb.Ks.as<uint64_t>(), nparts, nrec, pb.rec.as<uint64_t>(),
+        HIP_TRY(launch_part_totals(pb.Hs.as<uint64_t>(), pb.Ks.as<uint64_t>(), nparts, nwg, pb.rec.as<uint64_t>(),
                                    pb.kmer.as<uint64_t>(), pb.off.as<uint64_t>(), s));
     } else {
         HIP_TRY(hipMemsetAsync(pb.rec.p, 0, ((uint64_t)nparts + 1) * 8, s));
@@ -133,16 +133,16 @@ int part_count(PartBufs &pb, int W, const uint64_t *recs, uint64_t nrec, int mod
 }
 
 // Writes the records grouped by part (parts in order) into out.
-int part_scatter(PartBufs &pb, int W, const uint64_t *recs, int mode, uint32_t G, const uint32_t *table, uint64_t *out,
-                 hipStream_t s) {
+int part_scatter(PartBufs &pb, int mode, uint32_t G, const uint32_t *table, uint64_t *out, hipStream_t s) {
+    if (!pb.src.nrec) return FK_OK;
     if (pb.global) {
         FK_TRY(ensure(pb.cursor, ((uint64_t)pb.nparts + 1) * 8));
         HIP_TRY(hipMemsetAsync(pb.cursor.p, 0, ((uint64_t)pb.nparts + 1) * 8, s));
-        HIP_TRY(launch_part_scatter_global(W, recs, pb.nrec, mode, G, table, pb.nparts, pb.off.as<uint64_t>(),
+        HIP_TRY(launch_part_scatter_global(pb.src, mode, G, table, pb.nparts, pb.off.as<uint64_t>(),
                                            pb.cursor.as<uint64_t>(), out, s));
         return FK_OK;
     }
-    HIP_TRY(launch_part_scatter(W, recs, pb.nrec, mode, G, table, pb.nparts, pb.Hs.as<uint64_t>(), out, s));
+    HIP_TRY(launch_part_scatter(pb.src, mode, G, table, pb.nparts, pb.Hs.as<uint64_t>(), out, s));
     return FK_OK;
 }
 
@@ -234,8 +234,6 @@ struct fk_ctx {
     // streamed map (fused path): fk_ingest maps every tile whose bytes (and halo) have landed
     bool pm_active = false;     // the current input is being mapped while it is copied
     uint64_t pm_tiles = 0;      // tiles [0, pm_tiles) launched
-    uint64_t pm_rec_cap = 0;    // smallest record capacity any launch used
-    uint64_t pm_status_tiles = 0;  // look-back words allocated and zeroed
     bool pm_last_seen = false;  // an fk_ingest with last = 1 launched the final tiles
     const uint8_t *d_fasta = nullptr;
     uint64_t n_fasta = 0;
@@ -245,6 +243,9 @@ struct fk_ctx {
     DevBuf tile_last_nl, tile_off, npos_dev, codes, valid;
     // signature
     DevBuf records, counters, sig_status, sig_kmers;
+    DevBuf tcnt;                  // fused map: records per tile (tiled record layout)
+    bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
+    uint64_t rec_tiles = 0;       // tiles of the tiled layout
     uint64_t nrec = 0, nkmers = 0;
     bool mapped = false;
     // destination partition (n_ranks > 1)
@@ -451,7 +452,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
-                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers,
+                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
@@ -537,12 +538,14 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
     const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
     if (end <= c->pm_tiles) return FK_OK;
+    if (c->tcnt.bytes < end * 4 || c->records.bytes < end * map_fused_tcap() * c->W * 8)
+        return set_err(FK_E_STATE, "streamed map: %llu tiles exceed the reserved record slots",
+                       (unsigned long long)end);
     hipStream_t s = c->stream;
     if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
-                             end - c->pm_tiles, final_ ? end - 1 : ~0ull, c->fm, c->records.as<uint64_t>(),
-                             c->pm_rec_cap, c->sig_status.as<uint64_t>(), c->counters.as<unsigned long long>(), s,
-                             c->fused_probe));
+                             end - c->pm_tiles, c->fm, c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(),
+                             c->counters.as<unsigned long long>(), s, c->fused_probe));
     c->pm_tiles = end;
     if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
     return FK_OK;
@@ -573,8 +576,6 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
         c->pm_active = premap_eligible(c);
         c->pm_tiles = 0;
-        c->pm_status_tiles = 0;
-        c->pm_rec_cap = ~0ull;
         c->pm_last_seen = false;
     } else if (c->pm_last_seen) {
         c->pm_active = false;  // appending after the final tiles: fk_map maps the whole input
@@ -586,25 +587,15 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     }
     c->d_fasta = c->fasta_own.as<uint8_t>();
     if (c->pm_active) {
+        // record slots and per-tile counts of every tile this input can hold (kept on growth)
         const uint64_t tiles = (need + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
-        if (c->pm_status_tiles < tiles) {  // look-back words: kept, the new ones zeroed
-            const uint64_t want = std::max<uint64_t>(tiles, 2 * c->pm_status_tiles);
-            FK_TRY(grow_keep(c->sig_status, want * 8, c->pm_status_tiles * 8, s));
-            HIP_TRY(hipMemsetAsync(c->sig_status.as<uint64_t>() + c->pm_status_tiles, 0,
-                                   (want - c->pm_status_tiles) * 8, s));
-            c->pm_status_tiles = want;
-        }
+        if (c->tcnt.bytes < tiles * 4) FK_TRY(grow_keep(c->tcnt, tiles * 4, c->tcnt.bytes, s));
+        const uint64_t rec_need = tiles * map_fused_tcap() * c->W * 8;
+        if (c->records.bytes < rec_need) FK_TRY(grow_keep(c->records, rec_need, c->records.bytes, s));
         if (fresh) {
             FK_TRY(ensure(c->counters, 64));
             HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
         }
-        const uint64_t cap_need = std::max<uint64_t>(need / 6, 4096);
-        if (c->records.bytes < cap_need * c->W * 8) {
-            // records of the tiles mapped so far are kept; a launch that ran with
-            // a smaller capacity is caught by fk_map through pm_rec_cap
-            FK_TRY(grow_keep(c->records, cap_need * c->W * 8, c->records.bytes, s));
-        }
-        c->pm_rec_cap = std::min<uint64_t>(c->pm_rec_cap, c->records.bytes / (c->W * 8));
     }
     uint8_t *dst = c->fasta_own.as<uint8_t>() + have;
     hipPointerAttribute_t attr{};
@@ -653,7 +644,11 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
     DeviceGuard dg_(c->device);
     if (!c->ingest_fresh && c->d_fasta) return set_err(FK_E_STATE, "fk_ingest_reserve inside a streamed input");
     FK_TRY(ensure(c->fasta_own, total_bytes));
-    if (premap_eligible(c)) FK_TRY(ensure(c->records, std::max<uint64_t>(total_bytes / 6, 4096) * c->W * 8));
+    if (premap_eligible(c)) {
+        const uint64_t tiles = (total_bytes + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
+        FK_TRY(ensure(c->records, tiles * map_fused_tcap() * c->W * 8));
+        FK_TRY(ensure(c->tcnt, tiles * 4));
+    }
     return FK_OK;
 }
 
@@ -721,40 +716,41 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     *ok = false;
     const uint64_t tile = fm_tile_bytes(c->fused_nt);
     const uint64_t ntiles = (n + tile - 1) / tile;
-    FK_TRY(ensure(c->sig_status, ntiles * 8));
+    FK_TRY(ensure(c->tcnt, ntiles * 4));
     FK_TRY(ensure(c->counters, 64));
-    uint64_t rec_cap = std::max<uint64_t>(n / 6, 4096);
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        FK_TRY(ensure(c->records, rec_cap * c->W * 8));
-        rec_cap = c->records.bytes / (c->W * 8);
-        HIP_TRY(hipEventRecord(c->ev[2], s));
-        HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
-        HIP_TRY(hipMemsetAsync(c->sig_status.p, 0, ntiles * 8, s));
-        HIP_TRY(hipEventRecord(c->ev[10], s));
-        HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, ntiles - 1, c->fm,
-                                 c->records.as<uint64_t>(), rec_cap, c->sig_status.as<uint64_t>(),
-                                 c->counters.as<unsigned long long>(), s, c->fused_probe));
-        HIP_TRY(hipEventRecord(c->ev[11], s));
-        HIP_TRY(hipEventRecord(c->ev[3], s));
-        uint64_t h[4] = {0, 0, 0, 0};
-        HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        c->stats.fused_fallback = h[2];
-        if (h[2]) return FK_OK;  // fallback
-        c->nrec = h[0];
-        c->nkmers = h[1];
-        c->stats.positions = h[3];
-        if (c->nrec <= rec_cap) {
-            *ok = true;
-            break;
-        }
-        rec_cap = c->nrec;
-    }
+    FK_TRY(ensure(c->records, ntiles * map_fused_tcap() * c->W * 8));
+    HIP_TRY(hipEventRecord(c->ev[2], s));
+    HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
+    HIP_TRY(hipEventRecord(c->ev[10], s));
+    HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, c->fm,
+                             c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(), c->counters.as<unsigned long long>(),
+                             s, c->fused_probe));
+    HIP_TRY(hipEventRecord(c->ev[11], s));
+    HIP_TRY(hipEventRecord(c->ev[3], s));
+    uint64_t h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stats.fused_fallback = h[2];
+    if (h[2]) return FK_OK;  // fallback
+    c->nrec = h[0];
+    c->nkmers = h[1];
+    c->stats.positions = h[3];
+    c->rec_tiled = true;
+    c->rec_tiles = ntiles;
+    *ok = true;
     c->stats.ms_parse = 0.0;
     c->stats.ms_signature = ev_ms(c->ev[2], c->ev[3]);
     c->stats.ms_encode_kernel = 0.0;
     c->stats.ms_signature_kernel = ev_ms(c->ev[10], c->ev[11]);
     return FK_OK;
+}
+
+// the records of the last fk_map as a partition source
+static RecSrc map_src(const fk_ctx *c) {
+    if (c->rec_tiled)
+        return tiled_src(c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(), c->nrec, c->rec_tiles, map_fused_tcap(),
+                         c->W);
+    return dense_src(c->records.as<uint64_t>(), c->nrec, c->W);
 }
 
 FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
@@ -768,6 +764,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     c->stats = fk_stats{};
     c->stats.fasta_bytes = n;
     c->nrec = c->nkmers = 0;
+    c->rec_tiled = false;
 
     // 0. fused parse + signature (streamed by fk_ingest, or one launch here); the
     // two-kernel path below maps the inputs the fused kernel hands back
@@ -780,8 +777,10 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         c->stats.fused_fallback = h[2];
-        if (!h[2] && h[0] <= c->pm_rec_cap) {
+        if (!h[2]) {
             fused_ok = true;
+            c->rec_tiled = true;
+            c->rec_tiles = c->pm_tiles;
             c->nrec = h[0];
             c->nkmers = h[1];
             c->stats.positions = h[3];
@@ -789,8 +788,6 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
             // map stream from the first to the last launch, waits for the landing segments included
             c->stats.ms_signature = ev_ms(c->ev[10], c->ev[11]);
             c->stats.ms_signature_kernel = c->stats.ms_signature;
-        } else if (!h[2]) {
-            FK_TRY(map_fused(c, n, &fused_ok));  // record capacity: remap the resident input at once
         }
         c->pm_active = false;
     } else if (c->fused && n && map_fused_supported(c->cfg.k, c->cfg.m, (uint32_t)c->Bc)) {
@@ -893,8 +890,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
         c->grp_rec.assign(nparts, 0);
         c->grp_kmer.assign(nparts, 0);
         if (c->nrec) {
-            FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G,
-                              c->grp_table.as<uint32_t>(), nparts, c->ws, s));
+            FK_TRY(part_count(c->dest, map_src(c), 0, c->G, c->grp_table.as<uint32_t>(), nparts, c->ws, s));
             HIP_TRY(hipMemcpyAsync(c->grp_rec.data(), c->dest.rec.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipMemcpyAsync(c->grp_kmer.data(), c->dest.kmer.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
@@ -904,7 +900,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     } else if (c->G == 1) {
         c->send_counts[0] = c->nrec;
     } else if (c->nrec) {
-        FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, owner_table(c), c->G, c->ws, s));
+        FK_TRY(part_count(c->dest, map_src(c), 0, c->G, owner_table(c), c->G, c->ws, s));
         HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest.rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
@@ -925,12 +921,14 @@ FK_EXPORT int fk_map_emit(fk_ctx *c, void *d_send, uint64_t cap_records) {
     const double t0 = now_ms();
     hipStream_t s = c->stream;
     if (c->grouped) {
-        FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, c->grp_table.as<uint32_t>(),
-                            (uint64_t *)d_send, s));
-    } else if (c->G == 1) {
+        FK_TRY(part_scatter(c->dest, 0, c->G, c->grp_table.as<uint32_t>(), (uint64_t *)d_send, s));
+    } else if (c->G == 1 && !c->rec_tiled) {
         HIP_TRY(hipMemcpyAsync(d_send, c->records.p, c->nrec * c->W * 8, hipMemcpyDeviceToDevice, s));
+    } else if (c->G == 1) {  // the fused map's tiles, made dense
+        FK_TRY(part_count(c->dest, map_src(c), 0, 1, nullptr, 1, c->ws, s));
+        FK_TRY(part_scatter(c->dest, 0, 1, nullptr, (uint64_t *)d_send, s));
     } else {
-        FK_TRY(part_scatter(c->dest, c->W, c->records.as<uint64_t>(), 0, c->G, owner_table(c), (uint64_t *)d_send, s));
+        FK_TRY(part_scatter(c->dest, 0, c->G, owner_table(c), (uint64_t *)d_send, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
     c->stats.ms_total += now_ms() - t0;
@@ -946,7 +944,7 @@ FK_EXPORT int fk_map_bin_kmers(fk_ctx *c, uint64_t *kmers_per_bin) {
     DeviceGuard dg_(c->device);
     if (!c->mapped) return set_err(FK_E_STATE, "fk_map_bin_kmers before fk_map");
     hipStream_t s = c->stream;
-    FK_TRY(part_count(c->binhist, c->W, c->records.as<uint64_t>(), c->nrec, 1, 1, nullptr, (uint32_t)c->Bc, c->ws, s));
+    FK_TRY(part_count(c->binhist, map_src(c), 1, 1, nullptr, (uint32_t)c->Bc, c->ws, s));
     HIP_TRY(hipMemcpyAsync(kmers_per_bin, c->binhist.kmer.p, (uint64_t)c->Bc * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return FK_OK;
@@ -1007,8 +1005,7 @@ FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_
         if (c->G == 1) {
             c->send_counts[0] = c->nrec;
         } else if (c->nrec) {
-            FK_TRY(part_count(c->dest, c->W, c->records.as<uint64_t>(), c->nrec, 0, c->G, owner_table(c), c->G, c->ws,
-                              s));
+            FK_TRY(part_count(c->dest, map_src(c), 0, c->G, owner_table(c), c->G, c->ws, s));
             HIP_TRY(hipMemcpyAsync(c->send_counts.data(), c->dest.rec.p, c->G * 8, hipMemcpyDeviceToHost, s));
         }
     }
@@ -1301,16 +1298,15 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     return FK_OK;
 }
 
-FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
-    if (!c) return set_err(FK_E_INVALID, "null ctx");
-    DeviceGuard dg_(c->device);
-    if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
+// reduce of the records of `src` (all owned by this rank): partition by local bin, then count
+static int reduce_src(fk_ctx *c, const RecSrc &src) {
+    const uint64_t nrecv = src.nrec;
     const double t0 = now_ms();
     hipStream_t s = c->stream;
     c->have_result = false;
     const uint32_t nlb = c->nlb;
     HIP_TRY(hipEventRecord(c->ev[4], s));
-    FK_TRY(part_count(c->part, c->W, (const uint64_t *)d_recv, nrecv, 1, c->G, local_table(c), nlb, c->ws, s));
+    FK_TRY(part_count(c->part, src, 1, c->G, local_table(c), nlb, c->ws, s));
     std::vector<uint64_t> brec(nlb), bkm(nlb);
     if (nlb) {
         HIP_TRY(hipMemcpyAsync(brec.data(), c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
@@ -1332,10 +1328,17 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
     build_chunks(nlb, ranges, chunks, bcb);
     FK_TRY(ensure(c->precs, nrecv * c->W * 8));
     FK_TRY(upload_chunks(c, chunks, bcb));
-    FK_TRY(part_scatter(c->part, c->W, (const uint64_t *)d_recv, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
+    FK_TRY(part_scatter(c->part, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
     HIP_TRY(hipEventRecord(c->ev[5], s));
     c->rsrc = c->precs.as<uint64_t>();
     return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
+}
+
+FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
+    if (nrecv && !d_recv) return set_err(FK_E_INVALID, "null receive buffer");
+    return reduce_src(c, dense_src((const uint64_t *)d_recv, nrecv, c->W));
 }
 
 FK_EXPORT int fk_set_grouped_emit(fk_ctx *c, int32_t enable) {
@@ -1409,7 +1412,8 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     if (c->G != 1) return set_err(FK_E_STATE, "fk_finish is the single-rank path; use fk_map/fk_map_emit/fk_reduce");
     FK_TRY(fk_map(c, nullptr));
-    return fk_reduce(c, c->records.p, c->nrec);
+    DeviceGuard dg_(c->device);
+    return reduce_src(c, map_src(c));
 }
 
 // ---------------------------------------------------------------------------

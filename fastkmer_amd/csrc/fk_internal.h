@@ -64,37 +64,55 @@ hipError_t launch_superkmers(int W, const uint32_t *codes, const uint32_t *valid
 hipError_t launch_fill_u64(uint64_t *p, uint64_t n, uint64_t v, hipStream_t s);
 
 // ---- fused parse + signature (fk_map_fused.inc): FASTA bytes -> records in one kernel
-// for (k, m) with an instantiation and b <= 8192; tiles of fm_tile_bytes(nth) FASTA bytes
-// (nth = 256 or 512 threads), status[] = look-back words (zeroed), counters[4] =
-// records (set by last_tile), k-mers, fallback flag, positions.
+// for (k, m) with an instantiation; tiles of fm_tile_bytes(nth) FASTA bytes (nth = 256 or 512
+// threads).  Tile t's records go to records + t * map_fused_tcap() * W words, their count to
+// tcnt[t]; counters[4] (zeroed) = records, k-mers, fallback flags, positions.
 bool map_fused_supported(int k, int m, uint32_t nbins);
 uint64_t fm_tile_bytes(int nth);
 uint64_t fm_span_bytes(int nth);
+uint32_t map_fused_tcap();
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
-                            uint64_t ntiles, uint64_t last_tile, FastMod fm, uint64_t *records, uint64_t rec_cap,
-                            uint64_t *status, unsigned long long *counters, hipStream_t s, int probe = 0);
+                            uint64_t ntiles, FastMod fm, uint64_t *records, uint32_t *tcnt,
+                            unsigned long long *counters, hipStream_t s, int probe = 0);
+
+// ---- records to partition: dense (tcnt == null: nrec records, cut into PART_TILE tiles) or
+// tiled, as the fused map writes them (tile t holds tcnt[t] records at rec + t * tcap * W).
+constexpr uint32_t PART_TILE = 4096;  // dense records per tile
+constexpr uint32_t PART_TPC = 4;      // tiles per partition workgroup (dense: 16384 records)
+struct RecSrc {
+    const uint64_t *rec;
+    const uint32_t *tcnt;  // null: dense
+    uint64_t nrec;         // records (the sum of tcnt when tiled)
+    uint64_t ntiles;
+    uint32_t tcap;         // record slots per tile
+    uint32_t W;            // u64 words per record
+};
+inline RecSrc dense_src(const uint64_t *rec, uint64_t nrec, int W) {
+    return RecSrc{rec, nullptr, nrec, (nrec + PART_TILE - 1) / PART_TILE, PART_TILE, (uint32_t)W};
+}
+inline RecSrc tiled_src(const uint64_t *rec, const uint32_t *tcnt, uint64_t nrec, uint64_t ntiles, uint32_t tcap,
+                        int W) {
+    return RecSrc{rec, tcnt, nrec, ntiles, tcap, (uint32_t)W};
+}
 
 // ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]
-// record partition by part = bin % G (mode 0) or bin / G (mode 1).  H, K:
-// nparts * part_workgroups(nrec) u32 each; Hs, Ks: their exclusive scans
+// H, K: nparts * part_workgroups(src) u32 each; Hs, Ks: their exclusive scans
 // (one more entry, the total).
-constexpr uint32_t PART_CHUNK = 16384;  // records per partition workgroup
 constexpr uint32_t PART_MAX = 12288;    // parts per partition pass (LDS histogram)
-uint32_t part_workgroups(uint64_t nrec);
+uint32_t part_workgroups(const RecSrc &src);
 // table: optional bin -> part map (size-aware placement); null: the formula
-hipError_t launch_part_hist(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, const uint32_t *table,
-                            uint32_t nparts, uint32_t *H, uint32_t *K, hipStream_t s);
-hipError_t launch_part_totals(const uint64_t *Hs, const uint64_t *Ks, uint32_t nparts, uint64_t nrec,
+hipError_t launch_part_hist(const RecSrc &src, int mode, uint32_t G, const uint32_t *table, uint32_t nparts,
+                            uint32_t *H, uint32_t *K, hipStream_t s);
+hipError_t launch_part_totals(const uint64_t *Hs, const uint64_t *Ks, uint32_t nparts, uint32_t nwg,
                               uint64_t *part_rec, uint64_t *part_kmer, uint64_t *part_off, hipStream_t s);
-hipError_t launch_part_scatter(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G, const uint32_t *table,
-                               uint32_t nparts, const uint64_t *Hs, uint64_t *out, hipStream_t s);
+hipError_t launch_part_scatter(const RecSrc &src, int mode, uint32_t G, const uint32_t *table, uint32_t nparts,
+                               const uint64_t *Hs, uint64_t *out, hipStream_t s);
 // nparts > PART_MAX: totals by global atomics (part_rec/part_kmer zeroed), scatter by per-part cursors
-hipError_t launch_part_hist_global(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G,
-                                   const uint32_t *table, uint32_t nparts, uint64_t *part_rec, uint64_t *part_kmer,
-                                   hipStream_t s);
-hipError_t launch_part_scatter_global(int W, const uint64_t *rec, uint64_t nrec, int mode, uint32_t G,
-                                      const uint32_t *table, uint32_t nparts, const uint64_t *part_off,
-                                      uint64_t *part_cursor, uint64_t *out, hipStream_t s);
+hipError_t launch_part_hist_global(const RecSrc &src, int mode, uint32_t G, const uint32_t *table, uint32_t nparts,
+                                   uint64_t *part_rec, uint64_t *part_kmer, hipStream_t s);
+hipError_t launch_part_scatter_global(const RecSrc &src, int mode, uint32_t G, const uint32_t *table,
+                                      uint32_t nparts, const uint64_t *part_off, uint64_t *part_cursor,
+                                      uint64_t *out, hipStream_t s);
 
 // ---- sorted count
 hipError_t launch_expand_hist(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
