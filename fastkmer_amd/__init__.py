@@ -52,7 +52,8 @@ class fk_stats(ctypes.Structure):
                [(n, ctypes.c_double) for n in
                 ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
                  "ms_signature_kernel")] + [("fused_map", ctypes.c_uint64), ("ms_h2d", ctypes.c_double),
-                                       ("fused_fallback", ctypes.c_uint64)]
+                                       ("fused_fallback", ctypes.c_uint64),
+                                       ("ht_spilled", ctypes.c_uint64), ("ht_rounds", ctypes.c_uint64)]
 
 
 _lib = None

@@ -103,7 +103,36 @@ def build(force: bool = False) -> str:
     if force or _stale(CLI, [os.path.join(CSRC, "fk_cli.cpp"), LIB]):
         _run(["g++", "-O2", "-std=c++17", "-o", CLI, os.path.join(CSRC, "fk_cli.cpp"),
               f"-L{os.path.dirname(LIB)}", "-lfastkmer", "-Wl,-rpath,$ORIGIN/../lib"])
+    build_jni(force)
     return LIB
+
+
+JNI_SRC = os.path.join(ROOT, "jni", "fastkmer_jni.c")
+JNI_LIB = os.path.join(PKG, "lib", "libfastkmer_jni.so")
+
+
+def jni_include_dirs() -> list[str]:
+    """JDK include directories ($JAVA_HOME or a JDK under /usr/lib/jvm), [] when no jni.h exists."""
+    homes = [os.environ.get("JAVA_HOME", "")]
+    if os.path.isdir("/usr/lib/jvm"):
+        homes += [os.path.join("/usr/lib/jvm", d) for d in sorted(os.listdir("/usr/lib/jvm"))]
+    for h in homes:
+        inc = os.path.join(h, "include") if h else ""
+        if inc and os.path.exists(os.path.join(inc, "jni.h")):
+            return [inc, os.path.join(inc, "linux")]
+    return []
+
+
+def build_jni(force: bool = False) -> str | None:
+    """The JNI shim (jni/fastkmer_jni.c) for skc.gpu.NativeKmerCounter, only where a JDK is
+    installed (this image has none: the shim is then not built)."""
+    incs = jni_include_dirs()
+    if not incs:
+        return None
+    if force or _stale(JNI_LIB, [JNI_SRC, LIB, os.path.join(ROOT, "include", "fastkmer.h")]):
+        _run(["gcc", "-O2", "-shared", "-fPIC", *[f"-I{d}" for d in incs], f"-I{os.path.join(ROOT, 'include')}",
+              JNI_SRC, f"-L{os.path.dirname(LIB)}", "-lfastkmer", "-Wl,-rpath,$ORIGIN", "-o", JNI_LIB])
+    return JNI_LIB
 
 
 if __name__ == "__main__":

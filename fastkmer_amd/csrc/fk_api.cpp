@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -244,6 +245,11 @@ struct fk_ctx {
     // signature
     DevBuf records, counters, sig_status, sig_kmers;
     DevBuf tcnt;                  // fused map: records per tile (tiled record layout)
+    // hash count in LDS tables (fk_count_lds.inc)
+    DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
+    double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
+    int lh_mode = 1;
+    int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
     uint64_t nrec = 0, nkmers = 0;
@@ -402,6 +408,10 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (fn && fn[0]) c->fused_nt = atoi(fn) == 256 ? 256 : 512;
     const char *fp = getenv("FASTKMER_FUSED_PROBE");
     if (fp && fp[0]) c->fused_probe = atoi(fp);
+    const char *lh = getenv("FASTKMER_LDS_HT");
+    if (lh && lh[0]) c->lh_mode = atoi(lh);
+    const char *lp = getenv("FASTKMER_LH_PROBE");
+    if (lp && lp[0]) c->lh_probe = atoi(lp);
     const char *cm = getenv("FASTKMER_COUNT_MODE");
     if (cm && cm[0]) c->count_mode = atoi(cm);
     if (cfg->device >= 0) {
@@ -453,6 +463,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt,
+                      &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
+                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
@@ -1192,6 +1204,139 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     return FK_OK;
 }
 
+// Hash count in LDS tables (fk_count_lds.inc): bins split into 2^f_b groups by
+// the records' signature fine hash, one workgroup per group, spill rounds until
+// every key is counted, then the bins' regions packed densely.  f_b is sized so
+// a group's expected distinct k-mers (k-mers x the last run's distinct ratio)
+// fill about half a table.
+static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std::vector<uint32_t> &bcb,
+                         const std::vector<uint64_t> &bin_kmers) {
+    hipStream_t s = c->stream;
+    const uint32_t nlb = c->nlb, nchunks = (uint32_t)chunks.size();
+    const double per_group = 4096.0 * 0.5;  // LH_TS slots, half full
+    std::vector<uint8_t> flog(nlb, 0);
+    std::vector<uint32_t> gbase(nlb + 1, 0);
+    std::vector<uint64_t> rec_base(nlb + 1, 0), km_base(nlb + 1, 0);
+    for (uint32_t lb = 0; lb < nlb; ++lb) {
+        const double want = (double)bin_kmers[lb] * c->lh_ratio / per_group;
+        int f = 0;
+        while (f < LH_MAX_FLOG && (double)(1u << f) < want) ++f;
+        flog[lb] = (uint8_t)f;
+        gbase[lb + 1] = gbase[lb] + (1u << f);
+        uint64_t nr = 0;
+        for (uint32_t ch = bcb[lb]; ch < bcb[lb + 1]; ++ch) nr += chunks[ch].rec_end - chunks[ch].rec_begin;
+        rec_base[lb + 1] = rec_base[lb] + nr;
+        km_base[lb + 1] = km_base[lb] + bin_kmers[lb];
+    }
+    const uint32_t ngroups = gbase[nlb];
+    const uint64_t nrec = rec_base[nlb], nkm = km_base[nlb];
+    // one upload: rec_base, km_base (u64), gbase (u32), flog (u8)
+    const size_t meta_bytes = (size_t)(nlb + 1) * 16 + (size_t)(nlb + 1) * 4 + nlb + 16;
+    std::vector<uint8_t> meta(meta_bytes);
+    std::memcpy(meta.data(), rec_base.data(), (nlb + 1) * 8);
+    std::memcpy(meta.data() + (nlb + 1) * 8, km_base.data(), (nlb + 1) * 8);
+    std::memcpy(meta.data() + (nlb + 1) * 16, gbase.data(), (nlb + 1) * 4);
+    std::memcpy(meta.data() + (nlb + 1) * 20, flog.data(), nlb);
+    FK_TRY(ensure(c->lh_meta, meta_bytes));
+    HIP_TRY(hipMemcpyAsync(c->lh_meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, s));
+    const uint64_t *d_rec_base = c->lh_meta.as<uint64_t>(), *d_km_base = d_rec_base + (nlb + 1);
+    const uint32_t *d_gbase = reinterpret_cast<const uint32_t *>(d_rec_base + 2 * (uint64_t)(nlb + 1));
+    const uint8_t *d_flog = reinterpret_cast<const uint8_t *>(d_gbase + (nlb + 1));
+    FK_TRY(ensure(c->lh_H, (uint64_t)nchunks * 64 * 8 + 64));
+    FK_TRY(ensure(c->lh_off, (uint64_t)nchunks * 64 * 8 + 64));
+    FK_TRY(ensure(c->lh_groups, (uint64_t)ngroups * sizeof(LhGroup) + 64));
+    FK_TRY(ensure(c->lh_recs, nrec * c->W * 8 + 64));
+    FK_TRY(ensure(c->lh_spill[0], nkm * 8 + 64));
+    FK_TRY(ensure(c->lh_okeys, nkm * 8 + 64));
+    FK_TRY(ensure(c->lh_ocnt, nkm * 4 + 64));
+    FK_TRY(ensure(c->misc, 64));
+    FK_TRY(ensure(c->bin_off, ((uint64_t)nlb + 1) * 8));
+    FK_TRY(ensure(c->table_off, ((uint64_t)nlb + 1) * 8));  // per-bin distinct counts
+    uint32_t *Hr = c->lh_H.as<uint32_t>(), *Hk = Hr + (uint64_t)nchunks * 64;
+    LhGroup *groups = c->lh_groups.as<LhGroup>();
+    HIP_TRY(launch_fine_partition(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->bin_chunk_begin.as<uint32_t>(),
+                                  nlb, d_flog, d_rec_base, d_km_base, d_gbase, Hr, Hk, c->lh_off.as<uint64_t>(),
+                                  groups, c->lh_recs.as<uint64_t>(), s));
+    unsigned long long *bin_cnt = c->table_off.as<unsigned long long>();
+    unsigned long long *sp_total = c->misc.as<unsigned long long>();
+    HIP_TRY(hipMemsetAsync(bin_cnt, 0, ((uint64_t)nlb + 1) * 8, s));
+    HIP_TRY(hipMemsetAsync(sp_total, 0, 8, s));
+    FK_TRY(ensure(c->lh_sp[0], (uint64_t)ngroups * 4 + 64));
+    HIP_TRY(launch_ht_combine(c->W, c->lh_recs.as<uint64_t>(), groups, nullptr, ngroups, c->cfg.k, 0,
+                              c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
+                              c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe));
+    uint64_t spilled = 0;
+    HIP_TRY(hipMemcpyAsync(&spilled, sp_total, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stats.ht_spilled = spilled;
+    // spill rounds: each spilled range is split by a salted key hash into sub-groups of about
+    // per_group keys, so one heavy signature (a group far beyond a table) takes one more round
+    // instead of one per table's worth of keys
+    std::vector<LhItem> prev, items;
+    {
+        std::vector<uint32_t> cnt(ngroups);
+        if (spilled) HIP_TRY(hipMemcpy(cnt.data(), c->lh_sp[0].p, (uint64_t)ngroups * 4, hipMemcpyDeviceToHost));
+        std::vector<LhGroup> hg;
+        if (spilled) {
+            hg.resize(ngroups);
+            HIP_TRY(hipMemcpy(hg.data(), groups, (uint64_t)ngroups * sizeof(LhGroup), hipMemcpyDeviceToHost));
+        }
+        for (uint32_t g = 0; spilled && g < ngroups; ++g)
+            if (cnt[g]) prev.push_back(LhItem{hg[g].km_begin, 0, cnt[g], hg[g].lbin, 0, 0});
+    }
+    int cur = 0, rounds = 1;
+    while (spilled) {
+        if (++rounds > 16) return set_err(FK_E_DEVICE, "hash count: spill rounds do not converge");
+        const int nxt = cur ^ 1;
+        items.clear();
+        uint64_t out = 0;
+        for (const LhItem &p : prev) {
+            int sl = 0;
+            while (sl < 16 && (double)(1u << sl) * per_group < (double)p.in_cnt) ++sl;
+            for (uint32_t sub = 0; sub < (1u << sl); ++sub) {
+                items.push_back(LhItem{p.in_base, out, p.in_cnt, p.lbin, sub, (uint32_t)sl});
+                out += p.in_cnt;  // an item spills at most its range's keys
+            }
+        }
+        const uint32_t ni = (uint32_t)items.size();
+        FK_TRY(ensure(c->lh_spill[nxt], out * 8 + 64));
+        FK_TRY(ensure(c->lh_items, (uint64_t)ni * sizeof(LhItem) + 64));
+        LhItem *d_items = c->lh_items.as<LhItem>();
+        FK_TRY(ensure(c->lh_sp[nxt], (uint64_t)ni * 4 + 64));
+        HIP_TRY(hipMemcpyAsync(d_items, items.data(), (uint64_t)ni * sizeof(LhItem), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(sp_total, 0, 8, s));
+        HIP_TRY(launch_ht_combine(c->W, c->lh_spill[cur].as<uint64_t>(), groups, d_items, ni, c->cfg.k,
+                                  (uint32_t)rounds, c->lh_spill[nxt].as<uint64_t>(), c->lh_sp[nxt].as<uint32_t>(),
+                                  sp_total, d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(),
+                                  c->lh_ocnt.as<uint32_t>(), s));
+        HIP_TRY(hipMemcpyAsync(&spilled, sp_total, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        prev.clear();
+        if (spilled) {
+            std::vector<uint32_t> cnt(ni);
+            HIP_TRY(hipMemcpy(cnt.data(), c->lh_sp[nxt].p, (uint64_t)ni * 4, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < ni; ++i)
+                if (cnt[i]) prev.push_back(LhItem{items[i].out_base, 0, cnt[i], items[i].lbin, 0, 0});
+        }
+        cur = nxt;
+    }
+    c->stats.ht_rounds = (uint64_t)rounds;
+    // dense output: bin_off = scan of the per-bin distinct counts
+    HIP_TRY(scan_excl_sum_u64(reinterpret_cast<const uint64_t *>(bin_cnt), c->bin_off.as<uint64_t>(), nlb,
+                              c->bin_off.as<uint64_t>() + nlb, c->ws, s));
+    uint64_t distinct = 0;
+    HIP_TRY(hipMemcpyAsync(&distinct, c->bin_off.as<uint64_t>() + nlb, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    FK_TRY(ensure(c->dense_keys, distinct * 8 + 64));
+    FK_TRY(ensure(c->dense_counts, distinct * 4 + 64));
+    HIP_TRY(launch_ht_gather(d_km_base, c->bin_off.as<uint64_t>(), nlb, c->lh_okeys.as<uint64_t>(),
+                             c->lh_ocnt.as<uint32_t>(), c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(),
+                             s));
+    c->distinct = distinct;
+    if (nkm) c->lh_ratio = std::min(1.0, std::max(0.02, (double)distinct / (double)nkm));
+    return FK_OK;
+}
+
 static int reduce_ht(fk_ctx *c, uint32_t nchunks, const std::vector<uint64_t> &bin_kmers) {
     hipStream_t s = c->stream;
     std::vector<uint64_t> toff(c->nlb + 1, 0);
@@ -1271,7 +1416,9 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
         max_bin = std::max(max_bin, bkm[lb]);
     }
     HIP_TRY(hipEventRecord(c->ev[6], s));
-    if (c->cfg.use_ht)
+    if (c->cfg.use_ht && c->lh_mode && c->KW == 1)
+        FK_TRY(reduce_ht_lds(c, chunks, bcb, bkm));
+    else if (c->cfg.use_ht)
         FK_TRY(reduce_ht(c, nchunks, bkm));
     else
         FK_TRY(reduce_sorted(c, nchunks, total_kmers, max_bin));

@@ -93,6 +93,12 @@ FK_HD uint32_t hash32(uint32_t key) {
 
 FK_HD uint32_t bin_of_signature(uint32_t sig, const FastMod &f) { return fastmod(hash32(sig), f); }
 
+// 6-bit "fine" hash of a signature, kept in record header bits 26..31: the
+// LDS hash count splits a bin's records into groups by it, and every
+// occurrence of a canonical k-mer has the same signature (the norm is
+// strand-symmetric), so a k-mer's occurrences all land in one group.
+FK_HD uint32_t fine_of_signature(uint32_t sig) { return (sig * 0x9E3779B1u) >> 26; }
+
 // ---- canonical k-mers (getOrientation + readFromKmer, package.scala:721-728,
 // 174-295): canonical = min(forward, reverse complement) as 2k-bit integers,
 // A=0..T=3, most significant base first.

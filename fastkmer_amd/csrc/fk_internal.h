@@ -26,8 +26,9 @@ constexpr int POS_PAD_WORDS = 64;  // zero words after the packed stream (halo r
 constexpr int SORT_CAP = 4096;   // keys per LDS-sorted bucket (u64 keys; half for 128-bit keys)
 constexpr int MAX_FINE_BITS = 15;
 
-// record header (low 32 bits of word 0): bin | (n-1) << 22
+// record header (low 32 bits of word 0): bin | (n-1) << 22 | fine_of_signature(sig) << 26
 constexpr int REC_BIN_BITS = 22;
+constexpr int REC_FINE_SHIFT = 26;
 constexpr uint32_t REC_BIN_MASK = (1u << REC_BIN_BITS) - 1u;
 
 struct Bucket {
@@ -169,6 +170,31 @@ hipError_t launch_ht_compact(int KW, const uint64_t *tkeys, const uint32_t *tcou
                              hipStream_t s);
 hipError_t launch_ht_bin_offsets(const uint64_t *slot_scan, const uint64_t *table_off, uint32_t nlbins,
                                  uint64_t total, uint64_t *bin_off, hipStream_t s);
+
+// ---- hash count in LDS tables (fk_count_lds.inc), k <= 32
+struct LhGroup {          // one (local bin, fine value) group of records
+    uint64_t rec_begin;   // first record in the fine-partitioned array
+    uint64_t km_begin;    // first k-mer slot (prefix of the groups' k-mers): round-1 spill range
+    uint32_t rec_count, km_count;
+    uint32_t lbin, pad;
+};
+constexpr int LH_MAX_FLOG = 6;  // fine-hash bits in a record header
+hipError_t launch_fine_partition(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
+                                 const uint32_t *bcb, uint32_t nlb, const uint8_t *flog, const uint64_t *rec_base,
+                                 const uint64_t *km_base, const uint32_t *gbase, uint32_t *Hr, uint32_t *Hk,
+                                 uint64_t *off, LhGroup *groups, uint64_t *out, hipStream_t s);
+struct LhItem {            // one work item of a spill round: the spilled keys of a group (or of an
+    uint64_t in_base;     // item of the previous round) whose salted key hash selects `sub`
+    uint64_t out_base;    // spill range of this item (in_cnt slots)
+    uint32_t in_cnt, lbin, sub, slog;
+};
+// items == null: round 1 over groups[0..n); else spill round over items[0..n)
+hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, const LhItem *items, uint32_t n,
+                             int k, uint32_t salt, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
+                             const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys, uint32_t *ocnt,
+                             hipStream_t s, int probe = 0);
+hipError_t launch_ht_gather(const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb, const uint64_t *okeys,
+                            const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt, hipStream_t s);
 
 // ---- synthetic input
 hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);

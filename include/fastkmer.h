@@ -74,6 +74,8 @@ typedef struct fk_stats {
     double ms_h2d;             /* last fk_ingest: host-to-device copy, first segment issued to last landed */
     uint64_t fused_fallback;   /* why the fused kernel handed the input back: 1 long line, 2 text before the
                                   first header, 4 halo too short, 8 too many records in a tile (0: none) */
+    uint64_t ht_spilled;       /* useHT LDS tables: keys the first round spilled (counted by later rounds) */
+    uint64_t ht_rounds;        /* useHT LDS tables: rounds until every key was counted */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

@@ -1,0 +1,109 @@
+/*
+ * fastkmer_jni.c -- JNI binding of the C ABI (include/fastkmer.h) for the
+ * Scala object skc.gpu.NativeKmerCounter (jni/skc/gpu/NativeKmerCounter.scala).
+ *
+ * It is the thin host layer a fastkmer maintainer adds so that
+ * SparkBinKmerCounter.executeJob (src/main/scala/skc/SparkBinKmerCounter.scala:989)
+ * calls the MI355X counter instead of the Spark map / reduceByKey / reduce closures
+ * (:1033-1043).  Every native method maps to one fk_* call; a negative FK_E_* return
+ * becomes a java.lang.RuntimeException carrying fk_last_error(), mirroring the
+ * reference, whose failures are exceptions that fail the Spark task (require at
+ * package.scala:182,185; ArrayIndexOutOfBounds for x = 0 at SBKC:508).
+ *
+ * Build (only where a JDK is installed; this image has none):
+ *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
+ *       jni/fastkmer_jni.c -Lfastkmer_amd/lib -lfastkmer -Wl,-rpath,'$ORIGIN' -o libfastkmer_jni.so
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "fastkmer.h"
+
+static void throw_fk(JNIEnv *env, int rc) {
+    char msg[768];
+    snprintf(msg, sizeof msg, "fastkmer error %d: %s", rc, fk_last_error());
+    jclass ex = (*env)->FindClass(env, "java/lang/RuntimeException");
+    if (ex) (*env)->ThrowNew(env, ex, msg);
+}
+
+static fk_ctx *ctx_of(jlong h) { return (fk_ctx *)(intptr_t)h; }
+
+/* def create(k, m, x, b, useHT, sequenceType, nRanks, rank, device): Long */
+JNIEXPORT jlong JNICALL Java_skc_gpu_NativeKmerCounter_00024_create(JNIEnv *env, jobject self, jint k, jint m, jint x,
+                                                                   jint b, jboolean use_ht, jint seq_type,
+                                                                   jint n_ranks, jint rank, jint device) {
+    (void)self;
+    fk_config cfg;
+    fk_config_init(&cfg);
+    cfg.k = k;
+    cfg.m = m;
+    cfg.x = x;
+    cfg.B = b;
+    cfg.use_ht = use_ht ? 1 : 0;
+    cfg.sequence_type = seq_type;
+    cfg.n_ranks = n_ranks;
+    cfg.rank = rank;
+    cfg.device = device;
+    fk_ctx *c = NULL;
+    const int rc = fk_create(&cfg, &c);
+    if (rc != FK_OK) {
+        throw_fk(env, rc);
+        return 0;
+    }
+    return (jlong)(intptr_t)c;
+}
+
+/* def ingest(h, fasta: java.nio.ByteBuffer (direct or file-mapped), n, last): Unit */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_ingest(JNIEnv *env, jobject self, jlong h, jobject buf,
+                                                                  jlong n, jboolean last) {
+    (void)self;
+    const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (!p || cap < n || n < 0) {
+        jclass ex = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+        if (ex) (*env)->ThrowNew(env, ex, "ingest needs a direct ByteBuffer holding n bytes");
+        return;
+    }
+    const int rc = fk_ingest(ctx_of(h), p, (size_t)n, last ? 1 : 0);
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
+/* def finish(h): Unit -- map, count (one rank) */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_finish(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    const int rc = fk_finish(ctx_of(h));
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
+/* def binSizes(h): Array[Long] -- distinct k-mers per bin */
+JNIEXPORT jlongArray JNICALL Java_skc_gpu_NativeKmerCounter_00024_binSizes(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    const int32_t nb = fk_num_bins(ctx_of(h));
+    jlongArray out = (*env)->NewLongArray(env, nb);
+    if (!out || nb <= 0) return out;
+    jlong *dst = (*env)->GetLongArrayElements(env, out, NULL);
+    const int rc = fk_bin_sizes(ctx_of(h), (uint64_t *)dst);
+    (*env)->ReleaseLongArrayElements(env, out, dst, 0);
+    if (rc != FK_OK) throw_fk(env, rc);
+    return out;
+}
+
+/* def writeBins(h, outDir): Unit -- the reference's bin<b> files */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_writeBins(JNIEnv *env, jobject self, jlong h,
+                                                                     jstring dir) {
+    (void)self;
+    const char *d = (*env)->GetStringUTFChars(env, dir, NULL);
+    if (!d) return;
+    const int rc = fk_write_bins(ctx_of(h), d);
+    (*env)->ReleaseStringUTFChars(env, dir, d);
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
+/* def destroy(h): Unit */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_destroy(JNIEnv *env, jobject self, jlong h) {
+    (void)env;
+    (void)self;
+    fk_destroy(ctx_of(h));
+}

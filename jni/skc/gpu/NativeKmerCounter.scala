@@ -1,0 +1,50 @@
+/*
+ * skc.gpu.NativeKmerCounter -- Scala side of jni/fastkmer_jni.c.
+ *
+ * The drop-in for the body of SparkBinKmerCounter.executeJob
+ * (src/main/scala/skc/SparkBinKmerCounter.scala:989-1046): one MI355X context per
+ * executor runs the map (getSuperKmers, :34-169), the bin shuffle (reduceByKey,
+ * :1034-1042) and the per-bin count (extractKXmers / extractKXmersHT, :428-660,
+ * :664-739) and writes the same bin<b> files.  TestConfiguration is the reference's
+ * skc.test.testutil.TestConfiguration (src/main/scala/skc/test/package.scala:16-42).
+ * Not compiled in this repository (no JVM in the image); see INTEGRATION.md.
+ */
+package skc.gpu
+
+import java.nio.channels.FileChannel
+import java.nio.file.{Paths, StandardOpenOption}
+
+import skc.test.testutil.TestConfiguration
+
+object NativeKmerCounter {
+  System.loadLibrary("fastkmer_jni") // libfastkmer_jni.so, linked against libfastkmer.so
+
+  @native def create(k: Int, m: Int, x: Int, b: Int, useHT: Boolean, sequenceType: Int,
+                     nRanks: Int, rank: Int, device: Int): Long
+  @native def ingest(h: Long, fasta: java.nio.ByteBuffer, n: Long, last: Boolean): Unit
+  @native def finish(h: Long): Unit
+  @native def binSizes(h: Long): Array[Long]
+  @native def writeBins(h: Long, outDir: String): Unit
+  @native def destroy(h: Long): Unit
+
+  /** The file is streamed in mapped windows of `window` bytes (fk_ingest appends them). */
+  def executeJob(configuration: TestConfiguration, device: Int = -1, window: Long = 1L << 30): Unit = {
+    val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
+      configuration.useHT, configuration.sequenceType, 1, 0, device)
+    try {
+      val ch = FileChannel.open(Paths.get(configuration.dataset), StandardOpenOption.READ)
+      try {
+        val size = ch.size()
+        if (size == 0L) ingest(h, java.nio.ByteBuffer.allocateDirect(0), 0L, true)
+        var off = 0L
+        while (off < size) {
+          val len = math.min(window, size - off)
+          ingest(h, ch.map(FileChannel.MapMode.READ_ONLY, off, len), len, off + len >= size)
+          off += len
+        }
+      } finally ch.close()
+      finish(h)
+      if (configuration.write) writeBins(h, configuration.outputDir)
+    } finally destroy(h)
+  }
+}

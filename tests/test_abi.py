@@ -142,3 +142,19 @@ def test_lpt_owners_matches_reference_rule(n):
 def test_lpt_owners_validation():
     with pytest.raises(fk.FastKmerError):
         fk.lpt_owners(np.zeros(4, dtype=np.uint64), 0)
+
+
+def test_jni_shim_matches_the_scala_natives_and_the_abi():
+    """jni/fastkmer_jni.c defines one JNI function per @native method of
+    skc.gpu.NativeKmerCounter and calls only symbols include/fastkmer.h declares
+    (the shim is compiled only where a JDK exists; this image has none)."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    c_src = open(os.path.join(root, "jni", "fastkmer_jni.c")).read()
+    scala = open(os.path.join(root, "jni", "skc", "gpu", "NativeKmerCounter.scala")).read()
+    natives = set(re.findall(r"@native def (\w+)\(", scala))
+    jni_funcs = set(re.findall(r"Java_skc_gpu_NativeKmerCounter_00024_(\w+)\(", c_src))
+    assert natives and natives == jni_funcs
+    declared = set(fk.header_functions())
+    used = set(re.findall(r"\b(fk_\w+)\(", c_src))
+    assert used and used <= declared, used - declared
