@@ -13,6 +13,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -76,33 +82,52 @@ int main(int argc, char **argv) {
     if (part == 1) printf("\t no. partition tasks: %d", ntasks);
     printf("\n");
 
-    FILE *f = fopen(input, "rb");
-    if (!f) {
+    // the input is memory-mapped and streamed to the device in windows (FASTdoop reads its
+    // splits the same way, SBKC:1009-1012): fk_ingest appends each window and the fused map
+    // runs over the tiles that have landed while the next window is in flight
+    const int fd = open(input, O_RDONLY);
+    if (fd < 0) {
         fprintf(stderr, "cannot open %s\n", input);
         return 1;
     }
-    std::vector<uint8_t> buf;
-    {
-        fseek(f, 0, SEEK_END);
-        long sz = ftell(f);
-        fseek(f, 0, SEEK_SET);
-        buf.resize(sz > 0 ? (size_t)sz : 0);
-        if (sz > 0 && fread(buf.data(), 1, (size_t)sz, f) != (size_t)sz) {
-            fprintf(stderr, "short read on %s\n", input);
-            fclose(f);
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) {
+        fprintf(stderr, "cannot stat %s\n", input);
+        close(fd);
+        return 1;
+    }
+    const size_t size = (size_t)sb.st_size;
+    const uint8_t *map = nullptr;
+    if (size) {
+        void *p = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (p == MAP_FAILED) {
+            fprintf(stderr, "cannot map %s\n", input);
+            close(fd);
             return 1;
         }
-        fclose(f);
+        (void)madvise(p, size, MADV_SEQUENTIAL);
+        map = (const uint8_t *)p;
     }
     fk_ctx *ctx = nullptr;
     if (fk_create(&cfg, &ctx) != FK_OK) {
         fprintf(stderr, "fk_create: %s\n", fk_last_error());
+        if (map) munmap((void *)map, size);
+        close(fd);
         return 1;
     }
+    const size_t window = (size_t)256 << 20;
     auto t0 = std::chrono::steady_clock::now();
-    int rc = fk_ingest(ctx, buf.data(), buf.size(), 1);
+    int rc = fk_ingest_reserve(ctx, size);
+    for (size_t off = 0; rc == FK_OK && (off < size || off == 0);) {
+        const size_t len = std::min(window, size - off);
+        rc = fk_ingest(ctx, map ? map + off : nullptr, len, off + len >= size ? 1 : 0);
+        off += len;
+        if (size == 0) break;
+    }
     if (rc == FK_OK) rc = fk_finish(ctx);
     auto t1 = std::chrono::steady_clock::now();
+    if (map) munmap((void *)map, size);
+    close(fd);
     if (rc != FK_OK) {
         fprintf(stderr, "fk_finish: %s\n", fk_last_error());
         fk_destroy(ctx);

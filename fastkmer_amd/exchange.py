@@ -239,8 +239,9 @@ def count_distributed_rounds(rc: RoundCounters, group=None, device=None) -> int:
 def execute_job_distributed(configuration, group=None, device=None, rounds=None):
     """SparkBinKmerCounter.executeJob (SBKC:989-1046) for one rank of a job.
 
-    Every rank reads the dataset, keeps its shard (fastkmer_amd.sharding),
-    maps, exchanges records with the other ranks and counts the bins it owns
+    Every rank reads only its shard of the dataset with positioned reads
+    (fastkmer_amd.sharding.read_shard: its ~size/world bytes plus the k - 1
+    positions after them, FASTdoop's split, SBKC:1009-1012), maps, exchanges records with the other ranks and counts the bins it owns
     (bin % world == rank); with ``configuration.write`` each rank writes its
     own ``bin<b>`` files into the shared output directory, as the Spark
     executors do.  The exchange runs in ``rounds`` overlapped rounds
@@ -248,14 +249,11 @@ def execute_job_distributed(configuration, group=None, device=None, rounds=None)
     counter (a KmerCounter, or a RoundCounters for R > 1).
     """
     import fastkmer_amd as fk
-    from fastkmer_amd.sharding import shard_fasta
+    from fastkmer_amd.sharding import read_shard
 
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    with open(configuration.dataset, "rb") as f:
-        data = f.read()
-    piece = shard_fasta(data, world, rank, configuration.sequenceType, configuration.k)
-    del data
+    piece = read_shard(configuration.dataset, world, rank, configuration.k).piece
     R = 1 if configuration.useCustomPartitioner else (default_rounds(world) if rounds is None else rounds)
     args = (configuration.k, configuration.m, configuration.x, configuration.max_b, configuration.useHT,
             configuration.sequenceType)

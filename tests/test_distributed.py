@@ -223,3 +223,90 @@ def test_execute_job_distributed_rccl(tmp_path, use_ht, rounds):
             assert sorted(x for x in got[name].split(b"\n") if x) == sorted(x for x in want[name].split(b"\n") if x)
         else:
             assert got[name] == want[name]
+
+
+# ---------------------------------------------------------------- per-rank file reads (CPU)
+
+def _fasta_variants():
+    rng = random.Random(77)
+
+    def reads(n, lo, hi, wrap=0, junk=b"", crlf=False, hdr=(5, 30)):
+        out = [junk]
+        for i in range(n):
+            s = "".join(rng.choice("ACGTN" if rng.random() < 0.05 else "ACGT") for _ in range(rng.randint(lo, hi)))
+            if wrap and s:
+                s = "\n".join(s[q:q + wrap] for q in range(0, len(s), wrap))
+            h = ">" + "".join(rng.choice("abcdef0123 ") for _ in range(rng.randint(*hdr)))
+            rec = f"{h}\n{s}\n"
+            out.append(rec.replace("\n", "\r\n").encode() if crlf else rec.encode())
+        return b"".join(out)
+
+    return {
+        "short_reads": fk.synth_fasta(1500, 100, 40_000, seed=3),
+        "wrapped_reads": reads(300, 20, 400, wrap=61),
+        "junk_first": reads(200, 50, 150, junk=b"some text\nmore ACGT text\n"),
+        "crlf": reads(200, 30, 120, crlf=True),
+        "long_headers": reads(150, 10, 200, hdr=(200, 3000)),
+        "one_long_record": _long_fasta(),
+        "empty_records": reads(100, 0, 3),
+    }
+
+
+@pytest.mark.parametrize("name", sorted(_fasta_variants()))
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_read_shard_counts_add_up(tmp_path, name, world):
+    from fastkmer_amd.sharding import read_shard
+    data = _fasta_variants()[name]
+    path = tmp_path / "in.fa"
+    path.write_bytes(data)
+    for k, m, st in [(28, 10, 0), (21, 9, 1)]:
+        whole = _all_counts(oracle.OracleResult(data, k, m, 256, st))
+        summed: dict = {}
+        for r in range(world):
+            sh = read_shard(str(path), world, r, k)
+            for key, c in _all_counts(oracle.OracleResult(sh.piece, k, m, 256, st)).items():
+                summed[key] = summed.get(key, 0) + c
+        assert summed == whole, (name, world, k)
+
+
+def _read_shard_worker(rank, world, port, path, k, q):
+    from fastkmer_amd.sharding import read_shard
+    _init(rank, world, port)
+    sh = read_shard(path, world, rank, k)
+    res = oracle.OracleResult(sh.piece, k, 10, 2048)
+    counts = _all_counts(res)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (sh.touched, counts))
+    if rank == 0:
+        q.put(gathered)
+    dist.destroy_process_group()
+
+
+def test_per_rank_reads_touch_only_their_range(tmp_path):
+    """World-size-2 gloo job: every rank reads only its n / world bytes plus one
+    record's worth (the k - 1 positions after its range and the scans placing its
+    ends), and the ranks' counts add up to the whole file's (the oracle's)."""
+    world, k = 2, 28
+    data = fk.synth_fasta(20_000, 100, 200_000, seed=9)
+    path = tmp_path / "reads.fa"
+    path.write_bytes(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_read_shard_worker, args=(r, world, port, str(path), k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # beyond its range a rank reads: the file's first byte, the first byte of the line holding its
+    # range start and one 256-byte scan step each way to place that line (a 114-byte record is
+    # shorter than one step), and the k - 1 positions after its range in one read of 2 (k - 1) + 64
+    one_record = 2 + 2 * 256 + 2 * (k - 1) + 64
+    summed: dict = {}
+    for touched, counts in got:
+        assert touched <= len(data) // world + one_record + 1, touched
+        for key, c in counts.items():
+            summed[key] = summed.get(key, 0) + c
+    assert summed == _all_counts(oracle.OracleResult(data, k, 10, 2048))
