@@ -248,8 +248,8 @@ struct fk_ctx {
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
-    int lh_mode = 1;
-    int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
+    int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
+    int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
     uint64_t nrec = 0, nkmers = 0;
