@@ -1,0 +1,78 @@
+"""write=1 parity at the BASELINE sizes (the bin<b> writers of
+SBKC:550-606 (sorted, "EOF" trailer) and SBKC:715-734 (HT, no trailer)),
+through the C-ABI (needs a GPU).
+
+* configs[0] (10 MB of 100 bp reads, k=28 m=10 x=3 B=2048): every bin<b> file
+  fk_write_bins writes is compared with the oracle's writer -- byte-identical
+  for useHT=0; for useHT=1 the same files with the same lines (the line order
+  is the reference's hash-table order, fastutil 7.2.0, unpinned; see DESIGN).
+* configs[1] (1 GB): fk_write_bins is timed (MB/s printed and checked
+  against a floor), then a seeded sample of bins is byte-compared with the
+  oracle's text for those bins, and every file's line count is checked
+  against the device bin sizes.
+"""
+import os
+import random
+import time
+
+import numpy as np
+import pytest
+
+import fastkmer_amd as fk
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+K, M, X, B = 28, 10, 3, 2048
+
+
+def _files(d):
+    return {f: open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d))}
+
+
+@pytest.mark.parametrize("use_ht", [False, True])
+def test_write_bins_configs0_every_file(tmp_path, use_ht):
+    fasta = fk.synth_fasta(10_000_000 // 114, 100, 1_000_000, seed=0x5EED)
+    ref = oracle.OracleResult(fasta, K, M, B)
+    with fk.KmerCounter(K, M, X, B, use_ht) as kc:
+        kc.ingest(fasta)
+        kc.finish()
+        kc.write_bins(str(tmp_path / "gpu"))
+    ref.write_bins(str(tmp_path / "ref"), sorted_eof=not use_ht)
+    got, exp = _files(tmp_path / "gpu"), _files(tmp_path / "ref")
+    assert sorted(got) == sorted(exp) and len(got) > 1000
+    if not use_ht:
+        bad = [f for f in exp if got[f] != exp[f]]
+        assert not bad, f"{len(bad)} files differ, e.g. {bad[:3]}"
+    else:
+        for f in exp:
+            assert not got[f].endswith(b"EOF")
+            assert sorted(got[f].splitlines()) == sorted(exp[f].splitlines()), f
+
+
+def test_write_bins_configs1_sampled_and_timed(tmp_path):
+    n_reads = 1_000_000_000 // 114
+    fasta = fk.synth_fasta(n_reads, 100, 100_000_000, seed=0x5EED)
+    with fk.KmerCounter(K, M, X, B) as kc:
+        kc.ingest(fasta)
+        kc.finish()
+        sizes = kc.bin_sizes()
+        out = tmp_path / "out"
+        t0 = time.perf_counter()
+        kc.write_bins(str(out))
+        dt = time.perf_counter() - t0
+    nbytes = sum(os.path.getsize(out / f) for f in os.listdir(out))
+    mbs = nbytes / dt / 1e6
+    print(f"\nfk_write_bins configs[1]: {nbytes / 1e6:.0f} MB in {len(os.listdir(out))} files, "
+          f"{dt:.2f} s = {mbs:.0f} MB/s")
+    assert mbs > 200  # device formatting + D2H + file writes; ~3.8 GB of text
+    files = sorted(os.listdir(out))
+    assert files == sorted(f"bin{b}" for b in np.nonzero(sizes)[0].tolist())
+    ref = oracle.OracleResult(fasta, K, M, B, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(sizes.astype(np.int64), ref.bin_sizes())
+    rng = random.Random(7)
+    for b in rng.sample(np.nonzero(sizes)[0].tolist(), 24):
+        assert (out / f"bin{b}").read_text() == ref.bin_text(b), b
+    for f in rng.sample(files, 64):  # one line per distinct k-mer, then "EOF"
+        text = (out / f).read_bytes()
+        assert text.endswith(b"EOF") and text.count(b"\n") == int(sizes[int(f[3:])])
