@@ -1156,14 +1156,24 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, s));
-        if (ntier[1]) {
+        uint64_t nlarge = ntier[1];
+        if (ntier[1] && c->KW == 1 && !c->force_large) {
+            // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
+            HIP_TRY(launch_bucket_count64_big(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[1], k,
+                                              c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                              c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
+                                              lists + nbuckets, s));
+            HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        if (nlarge) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
             HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              lists + nbuckets, s));
         }
-        c->stats.oversize_buckets = ntier[1];
+        c->stats.oversize_buckets = nlarge;
     } else {
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,

@@ -131,6 +131,9 @@ hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buck
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
                                  const uint32_t *list, hipStream_t s);
+hipError_t launch_bucket_count64_big(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nlist, int k,
+                                     uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+                                     unsigned long long *oversize, const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
