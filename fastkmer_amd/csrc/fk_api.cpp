@@ -208,6 +208,7 @@ struct fk_ctx {
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
     int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
+    int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
     bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
@@ -397,6 +398,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     const char *wc = getenv("FASTKMER_WAVE_CAP");
     if (wc && wc[0]) c->wave_cap = (uint32_t)atoi(wc);
     const char *f2 = getenv("FASTKMER_F2");
+    if (const char *hb = getenv("FASTKMER_HIST_BIN"); hb && hb[0]) c->hist_bin = atoi(hb);
     if (f2 && f2[0]) c->f2_bits = std::max(0, std::min(9, atoi(f2)));
     const char *bp = getenv("FASTKMER_WAVE_BPW");
     if (bp && bp[0]) c->wave_bpw = atoi(bp);
@@ -1066,11 +1068,16 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         const uint64_t nsc_all = (uint64_t)c->nlb << F1;
         FK_TRY(ensure(c->lp, ((uint64_t)nchunks << F1) * 4));
         FK_TRY(ensure(c->sc_total, nsc_all * 8));
-        HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
-        HIP_TRY(launch_expand_hist_sc(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F, F2,
-                                      c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
-        HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F1, c->lp.as<uint32_t>(),
-                                   c->sc_total.as<uint64_t>(), s));
+        if (c->hist_bin) {
+            HIP_TRY(launch_expand_hist_bin(c->KW, c->rsrc, c->chunks.as<Chunk>(), c->bin_chunk_begin.as<uint32_t>(),
+                                           c->nlb, k, F, F2, c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
+        } else {
+            HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
+            HIP_TRY(launch_expand_hist_sc(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F, F2,
+                                          c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
+            HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F1, c->lp.as<uint32_t>(),
+                                       c->sc_total.as<uint64_t>(), s));
+        }
     } else {
         FK_TRY(ensure(c->lp, (uint64_t)nchunks * ncell * 4));
         HIP_TRY(launch_expand_hist(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,

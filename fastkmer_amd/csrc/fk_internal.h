@@ -143,7 +143,11 @@ hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chu
                                    uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
                                    const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s);
 hipError_t launch_expand_hist_sc(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
-                                 int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);  // keys per wave-tier bucket (k_bucket_count64_wave)
+                                 int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);
+// one workgroup per local bin: cell totals and the per-chunk exclusive super-cell prefix in one pass
+hipError_t launch_expand_hist_bin(int KW, const uint64_t *rec, const Chunk *chunks, const uint32_t *bin_chunk_begin,
+                                  uint32_t nlbins, int k, int F, int F2, uint64_t *cell_total, uint32_t *hist_sc,
+                                  hipStream_t s);
 hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
                                       int period_bits, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
