@@ -207,6 +207,7 @@ struct fk_ctx {
     int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
     int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
+    uint32_t greedy_cap = 0;   // FASTKMER_GREEDY_CAP (probe): pack cells into buckets of up to this many keys (0 = wave_cap)
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
     int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
@@ -397,6 +398,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (el && el[0]) c->expand_levels = atoi(el);
     const char *wc = getenv("FASTKMER_WAVE_CAP");
     if (wc && wc[0]) c->wave_cap = (uint32_t)atoi(wc);
+    if (const char *gc = getenv("FASTKMER_GREEDY_CAP"); gc && gc[0]) c->greedy_cap = (uint32_t)atoi(gc);
     const char *f2 = getenv("FASTKMER_F2");
     if (const char *hb = getenv("FASTKMER_HIST_BIN"); hb && hb[0]) c->hist_bin = atoi(hb);
     if (f2 && f2[0]) c->f2_bits = std::max(0, std::min(9, atoi(f2)));
@@ -1114,7 +1116,8 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F, wave_cap, -1,
+        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F,
+                                           c->greedy_cap ? c->greedy_cap : wave_cap, -1,
                                            c->flags.as<uint32_t>(), s));
     else
         HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
