@@ -85,13 +85,13 @@ void release(DevBuf &b) {
 
 // Record partition (fk_partition.inc): histogram -> scan -> scatter.
 struct PartBufs {
-    DevBuf H, K, Hs, Ks;                  // per-workgroup histograms (column-major) and their scans
+    DevBuf H, K, Hs, Ts, KT;              // per-workgroup histograms and destinations (rows), segment sums
     DevBuf rec, kmer, off, cursor;        // per-part totals / offsets (device), cursor: global path only
     uint32_t nparts = 0;
     RecSrc src{};                         // the records counted (part_scatter reads the same)
     bool global = false;                  // nparts > PART_MAX: global-atomic kernels
     void release_all() {
-        for (DevBuf *b : {&H, &K, &Hs, &Ks, &rec, &kmer, &off, &cursor}) release(*b);
+        for (DevBuf *b : {&H, &K, &Hs, &Ts, &KT, &rec, &kmer, &off, &cursor}) release(*b);
     }
 };
 
@@ -117,13 +117,17 @@ int part_count(PartBufs &pb, const RecSrc &src, int mode, uint32_t G, const uint
     const uint64_t n = (uint64_t)nparts * nwg;
     FK_TRY(ensure(pb.H, n * 4));
     FK_TRY(ensure(pb.K, n * 4));
-    FK_TRY(ensure(pb.Hs, (n + 1) * 8));
-    FK_TRY(ensure(pb.Ks, (n + 1) * 8));
+    const uint64_t nt = (uint64_t)nparts * part_segments(nwg);
+    FK_TRY(ensure(pb.Hs, n * 8));
+    FK_TRY(ensure(pb.Ts, (nt + 1) * 8));
+    FK_TRY(ensure(pb.KT, nt * 8));
     if (n) {
         HIP_TRY(launch_part_hist(src, mode, G, table, nparts, pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), s));
-        HIP_TRY(scan_excl_sum_u32_to_u64(pb.H.as<uint32_t>(), pb.Hs.as<uint64_t>(), n, pb.Hs.as<uint64_t>() + n, ws, s));
-        HIP_TRY(scan_excl_sum_u32_to_u64(pb.K.as<uint32_t>(), pb.Ks.as<uint64_t>(), n, pb.Ks.as<uint64_t>() + n, ws, s));
-        HIP_TRY(launch_part_totals(pb.Hs.as<uint64_t>(), pb.Ks.as<uint64_t>(), nparts, nwg, pb.rec.as<uint64_t>(),
+        HIP_TRY(launch_part_segsum(pb.H.as<uint32_t>(), pb.K.as<uint32_t>(), nparts, nwg, pb.Ts.as<uint64_t>(),
+                                   pb.KT.as<uint64_t>(), s));
+        HIP_TRY(scan_excl_sum_u64(pb.Ts.as<uint64_t>(), pb.Ts.as<uint64_t>(), nt, pb.Ts.as<uint64_t>() + nt, ws, s));
+        HIP_TRY(launch_part_segfill(pb.H.as<uint32_t>(), pb.Ts.as<uint64_t>(), nparts, nwg, pb.Hs.as<uint64_t>(), s));
+        HIP_TRY(launch_part_totals(pb.Ts.as<uint64_t>(), pb.KT.as<uint64_t>(), nparts, nwg, pb.rec.as<uint64_t>(),
                                    pb.kmer.as<uint64_t>(), pb.off.as<uint64_t>(), s));
     } else {
         HIP_TRY(hipMemsetAsync(pb.rec.p, 0, ((uint64_t)nparts + 1) * 8, s));

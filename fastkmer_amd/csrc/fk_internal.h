@@ -80,6 +80,8 @@ hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n
 // tiled, as the fused map writes them (tile t holds tcnt[t] records at rec + t * tcap * W).
 constexpr uint32_t PART_TILE = 4096;  // dense records per tile
 constexpr uint32_t PART_TPC = 4;      // tiles per partition workgroup (dense: 16384 records)
+constexpr uint32_t PART_SEG = 64;     // partition workgroups per segment of the histogram scan
+inline uint32_t part_segments(uint32_t nwg) { return (nwg + PART_SEG - 1) / PART_SEG; }
 struct RecSrc {
     const uint64_t *rec;
     const uint32_t *tcnt;  // null: dense
@@ -104,6 +106,12 @@ uint32_t part_workgroups(const RecSrc &src);
 // table: optional bin -> part map (size-aware placement); null: the formula
 hipError_t launch_part_hist(const RecSrc &src, int mode, uint32_t G, const uint32_t *table, uint32_t nparts,
                             uint32_t *H, uint32_t *K, hipStream_t s);
+// row-major histograms H/K[wg * nparts + p] -> part-major segment sums T/KT[p * nseg + seg]
+hipError_t launch_part_segsum(const uint32_t *H, const uint32_t *K, uint32_t nparts, uint32_t nwg, uint64_t *T,
+                              uint64_t *KT, hipStream_t s);
+// scanned segment sums -> destinations Hs[wg * nparts + p]
+hipError_t launch_part_segfill(const uint32_t *H, const uint64_t *Ts, uint32_t nparts, uint32_t nwg, uint64_t *Hs,
+                               hipStream_t s);
 hipError_t launch_part_totals(const uint64_t *Hs, const uint64_t *Ks, uint32_t nparts, uint32_t nwg,
                               uint64_t *part_rec, uint64_t *part_kmer, uint64_t *part_off, hipStream_t s);
 hipError_t launch_part_scatter(const RecSrc &src, int mode, uint32_t G, const uint32_t *table, uint32_t nparts,
