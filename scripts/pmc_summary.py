@@ -24,14 +24,17 @@ for name, cs in sorted(acc.items()):
 if "--json" in sys.argv:
     import json
     out = sys.argv[sys.argv.index("--json") + 1]
-    stage = ("k_fasta_parse", "k_superkmers")
+    # the fused kernel when the run used it, else the two-kernel path
+    fused = any(name.startswith("k_map_fused") for name in acc)
+    stage = ("k_map_fused",) if fused else ("k_fasta_parse", "k_superkmers")
     per = {}
     for name, cs in acc.items():
         if any(name.startswith(s) for s in stage) and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024
             w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
             per[name] = {"fetch_size_bytes_raw": f, "write_size_bytes": w, "hbm_bytes_corrected": 2 * f + w}
-    json.dump({"source": sys.argv[1], "kernels": per,
+    json.dump({"source": sys.argv[1], "stage_kernel": "k_map_fused" if fused else "k_fasta_parse + k_superkmers",
+               "kernels": per,
                "encode_signature_hbm_bytes_per_launch": sum(v["hbm_bytes_corrected"] for v in per.values()),
                "correction": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md HBM section"},
               open(out, "w"), indent=1)
