@@ -118,7 +118,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--bytes-per-gpu", type=int, default=FASTA_BYTES_PER_GPU)
-    ap.add_argument("--cpu-sample-bytes", type=int, default=64_000_000)
+    ap.add_argument("--cpu-sample-bytes", type=int, default=160_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-leg", action="store_true", help="skip the pinned-host-input leg")
     ap.add_argument("--use-ht", action="store_true", help="hash count (extractKXmersHT, useHT=1)")
