@@ -17,7 +17,7 @@ for st in "$@"; do
 import csv, sys
 r = list(csv.DictReader(open(sys.argv[1])))
 for x in sorted(r, key=lambda x: -float(x['TotalDurationNs']))[:12]:
-    if 'synth' in x['Name'] or 'map_fused' in x['Name'] or 'part_' in x['Name']: continue
+    if 'synth' in x['Name'] or 'map_fused' in x['Name'] or 'part_hist' in x['Name']: continue
     print(f"   {x['Name'][:58]:58s} calls={x['Calls']:>4} avg_ms={float(x['AverageNs'])/1e6:.3f}")
 PY
 done
