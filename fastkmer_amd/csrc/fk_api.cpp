@@ -251,6 +251,7 @@ struct fk_ctx {
     // signature
     DevBuf records, counters, sig_status, sig_kmers;
     DevBuf tcnt;                  // fused map: records per tile (tiled record layout)
+    DevBuf rec_hdr;               // fused map: every record's header word, in the record's tile slot
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
@@ -470,7 +471,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
-                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt,
+                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
                       &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk, &c->grp_table,
@@ -558,13 +559,15 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
     const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
     if (end <= c->pm_tiles) return FK_OK;
-    if (c->tcnt.bytes < end * 4 || c->records.bytes < end * map_fused_tcap() * c->W * 8)
+    if (c->tcnt.bytes < end * 4 || c->records.bytes < end * map_fused_tcap() * c->W * 8 ||
+        c->rec_hdr.bytes < end * map_fused_tcap() * 4)
         return set_err(FK_E_STATE, "streamed map: %llu tiles exceed the reserved record slots",
                        (unsigned long long)end);
     hipStream_t s = c->stream;
     if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
-                             end - c->pm_tiles, c->fm, c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(),
+                             end - c->pm_tiles, c->fm, c->records.as<uint64_t>(), c->rec_hdr.as<uint32_t>(),
+                             c->tcnt.as<uint32_t>(),
                              c->counters.as<unsigned long long>(), s, c->fused_probe));
     c->pm_tiles = end;
     if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
@@ -612,6 +615,8 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         if (c->tcnt.bytes < tiles * 4) FK_TRY(grow_keep(c->tcnt, tiles * 4, c->tcnt.bytes, s));
         const uint64_t rec_need = tiles * map_fused_tcap() * c->W * 8;
         if (c->records.bytes < rec_need) FK_TRY(grow_keep(c->records, rec_need, c->records.bytes, s));
+        const uint64_t hdr_need = tiles * map_fused_tcap() * 4;
+        if (c->rec_hdr.bytes < hdr_need) FK_TRY(grow_keep(c->rec_hdr, hdr_need, c->rec_hdr.bytes, s));
         if (fresh) {
             FK_TRY(ensure(c->counters, 64));
             HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
@@ -667,6 +672,7 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
     if (premap_eligible(c)) {
         const uint64_t tiles = (total_bytes + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
         FK_TRY(ensure(c->records, tiles * map_fused_tcap() * c->W * 8));
+        FK_TRY(ensure(c->rec_hdr, tiles * map_fused_tcap() * 4));
         FK_TRY(ensure(c->tcnt, tiles * 4));
     }
     return FK_OK;
@@ -739,12 +745,13 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     FK_TRY(ensure(c->tcnt, ntiles * 4));
     FK_TRY(ensure(c->counters, 64));
     FK_TRY(ensure(c->records, ntiles * map_fused_tcap() * c->W * 8));
+    FK_TRY(ensure(c->rec_hdr, ntiles * map_fused_tcap() * 4));
     HIP_TRY(hipEventRecord(c->ev[2], s));
     HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
     HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, c->fm,
-                             c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(), c->counters.as<unsigned long long>(),
-                             s, c->fused_probe));
+                             c->records.as<uint64_t>(), c->rec_hdr.as<uint32_t>(), c->tcnt.as<uint32_t>(),
+                             c->counters.as<unsigned long long>(), s, c->fused_probe));
     HIP_TRY(hipEventRecord(c->ev[11], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     uint64_t h[4] = {0, 0, 0, 0};
@@ -769,7 +776,7 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
 static RecSrc map_src(const fk_ctx *c) {
     if (c->rec_tiled)
         return tiled_src(c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(), c->nrec, c->rec_tiles, map_fused_tcap(),
-                         c->W);
+                         c->W, c->rec_hdr.as<uint32_t>());
     return dense_src(c->records.as<uint64_t>(), c->nrec, c->W);
 }
 

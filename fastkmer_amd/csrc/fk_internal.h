@@ -73,7 +73,7 @@ uint64_t fm_tile_bytes(int nth);
 uint64_t fm_span_bytes(int nth);
 uint32_t map_fused_tcap();
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
-                            uint64_t ntiles, FastMod fm, uint64_t *records, uint32_t *tcnt,
+                            uint64_t ntiles, FastMod fm, uint64_t *records, uint32_t *hdrs, uint32_t *tcnt,
                             unsigned long long *counters, hipStream_t s, int probe = 0);
 
 // ---- records to partition: dense (tcnt == null: nrec records, cut into PART_TILE tiles) or
@@ -89,13 +89,14 @@ struct RecSrc {
     uint64_t ntiles;
     uint32_t tcap;         // record slots per tile
     uint32_t W;            // u64 words per record
+    const uint32_t *hdr;   // tiled: the records' header words in the same slots (null: read the records)
 };
 inline RecSrc dense_src(const uint64_t *rec, uint64_t nrec, int W) {
-    return RecSrc{rec, nullptr, nrec, (nrec + PART_TILE - 1) / PART_TILE, PART_TILE, (uint32_t)W};
+    return RecSrc{rec, nullptr, nrec, (nrec + PART_TILE - 1) / PART_TILE, PART_TILE, (uint32_t)W, nullptr};
 }
 inline RecSrc tiled_src(const uint64_t *rec, const uint32_t *tcnt, uint64_t nrec, uint64_t ntiles, uint32_t tcap,
-                        int W) {
-    return RecSrc{rec, tcnt, nrec, ntiles, tcap, (uint32_t)W};
+                        int W, const uint32_t *hdr = nullptr) {
+    return RecSrc{rec, tcnt, nrec, ntiles, tcap, (uint32_t)W, hdr};
 }
 
 // ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]
