@@ -11,4 +11,4 @@ timeout -k 10 400 python3 bench.py > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err
 rc=$?; cut -c1-400 $OUT/bench_$tag.json; [[ $rc -ne 0 ]] && exit $rc
 timeout -k 10 300 python3 bench.py --use-ht --no-cpu-baseline --no-host-leg > $OUT/bench_ht_$tag.json 2> $OUT/bench_ht_$tag.err
 rc=$?; cut -c1-300 $OUT/bench_ht_$tag.json; [[ $rc -ne 0 ]] && exit $rc
-bash scripts/prof_bench.sh $tag || exit 1
+bash scripts/prof_bench.sh $tag --no-host-leg || exit 1
