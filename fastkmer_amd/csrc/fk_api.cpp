@@ -211,6 +211,7 @@ struct fk_ctx {
     int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
     int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
+    int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
     uint32_t greedy_cap = 0;   // FASTKMER_GREEDY_CAP (probe): pack cells into buckets of up to this many keys (0 = wave_cap)
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
     int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
@@ -399,6 +400,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->scatter_wc = (sc && sc[0]) ? atoi(sc) : 1;
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
+    if (const char *x1 = getenv("FASTKMER_X2_L1"); x1 && x1[0]) c->x2_l1 = atoi(x1);
     const char *el = getenv("FASTKMER_EXPAND_LEVELS");
     if (el && el[0]) c->expand_levels = atoi(el);
     const char *wc = getenv("FASTKMER_WAVE_CAP");
@@ -1117,7 +1119,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
         HIP_TRY(launch_expand_two_level(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
                                         F2, c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->mid.as<uint64_t>(),
-                                        c->keys.as<uint64_t>(), s));
+                                        c->keys.as<uint64_t>(), s, c->x2_l1));
     } else {
         HIP_TRY(launch_expand_scatter(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,
                                       c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),

@@ -150,7 +150,8 @@ hipError_t launch_bucket_count128_wave(const uint64_t *keys, int F, const Bucket
                                        hipStream_t s);
 hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
                                    uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
-                                   const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s);
+                                   const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s,
+                                   int l1_threads = 0);
 hipError_t launch_expand_hist_sc(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
                                  int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);
 // one workgroup per local bin: cell totals and the per-chunk exclusive super-cell prefix in one pass

@@ -180,6 +180,30 @@ def test_long_sequence_type1_vs_oracle():
     assert_same_as_oracle(kc, ref)
 
 
+@pytest.mark.parametrize("l1", ["512", "1024"])
+def test_long_record_level1_kernels_vs_oracle(monkeypatch, l1):
+    # one long record, 60 % of it periodic blocks (a minimizer that never changes: records of 16
+    # k-mers), so records average > 9 k-mers and a 1024-record level-1 batch of k_expand_sc1024
+    # overflows its 8192-key stage and is stored from registers; both level-1 kernels against the
+    # oracle (FASTKMER_X2_L1 forces the kernel at any fan-out)
+    monkeypatch.setenv("FASTKMER_X2_L1", l1)
+    rng = random.Random(11)
+    parts = []
+    for blk in range(60):
+        if blk % 5 < 3:
+            unit = "".join(rng.choice("ACGT") for _ in range(rng.randint(5, 9)))
+            parts.append((unit * (25_000 // len(unit) + 1))[:25_000])
+        else:
+            parts.append("".join(rng.choice("ACGT") for _ in range(25_000)))
+    seq = "".join(parts)
+    fasta = (">chrL\n" + "\n".join(seq[q:q + 80] for q in range(0, len(seq), 80)) + "\n").encode()
+    kc = run_counter(fasta, 28, 10, 3, 64, False, sequence_type=1)
+    ref = oracle.OracleResult(fasta, 28, 10, 64, 1)
+    st = kc.stats()
+    assert st["kmers"] == ref.total_kmers and st["kmers"] > 9.0 * st["superkmers"]
+    assert_same_as_oracle(kc, ref)
+
+
 def test_large_bucket_path_vs_oracle(monkeypatch):
     # every bucket through the streaming global-memory sort (k_bucket_sort_large)
     monkeypatch.setenv("FASTKMER_DEBUG_LARGE_BUCKETS", "1")
@@ -400,6 +424,7 @@ def test_big_bins_two_level_vs_oracle():
     {"FASTKMER_EXPAND_LEVELS": "1", "FASTKMER_DEBUG_SCATTER": "0"},  # plain scatter
     {"FASTKMER_WAVE_CAP": "256", "FASTKMER_WAVE_BPW": "1"},
     {"FASTKMER_WAVE_CAP": "128", "FASTKMER_WAVE_BPW": "2", "FASTKMER_DEBUG_CELL_TARGET": "64"},
+    {"FASTKMER_X2_L1": "1024"},                                      # 1024-record level-1 batches
 ])
 def test_count_variants_identical(monkeypatch, env):
     # every count-stage variant gives the default path's result, bit for bit
