@@ -267,6 +267,8 @@ struct fk_ctx {
     // reduce
     PartBufs dest, part, binhist;  // record partition by destination rank (fk_map) / by local bin (fk_reduce)
     DevBuf precs, chunks, bin_chunk_begin;
+    std::vector<uint32_t> h_bcb;  // bin_chunk_begin on the host (the last uploaded chunk table)
+    DevBuf hpieces, hpiece_first, hpiece_tot;  // k_expand_hist_piece: bins split into pieces of chunks
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_total;
@@ -476,7 +478,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
                       &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
-                      &c->precs, &c->chunks, &c->bin_chunk_begin, &c->chunk_nk, &c->grp_table,
+                      &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
@@ -1083,7 +1085,37 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         const uint64_t nsc_all = (uint64_t)c->nlb << F1;
         FK_TRY(ensure(c->lp, ((uint64_t)nchunks << F1) * 4));
         FK_TRY(ensure(c->sc_total, nsc_all * 8));
-        if (c->hist_bin) {
+        // bins split into pieces of chunks so that ~HIST_PIECES workgroups balance over the CUs (one
+        // workgroup per bin waits for the largest bin when bins are few and large)
+        constexpr double HIST_PIECES = 1024.0;
+        std::vector<uint32_t> pieces, first;
+        bool split = false;
+        if (c->hist_bin && nchunks && c->h_bcb.size() == (size_t)c->nlb + 1) {
+            for (uint32_t lb = 0; lb < c->nlb; ++lb) {
+                const uint32_t cb = c->h_bcb[lb], ce = c->h_bcb[lb + 1], nc = ce - cb;
+                const uint32_t P = std::max(1u, std::min(nc, (uint32_t)(HIST_PIECES * nc / nchunks + 0.5)));
+                const uint32_t f = (uint32_t)(pieces.size() / 4);
+                for (uint32_t q = 0; q < P; ++q) {
+                    pieces.insert(pieces.end(), {lb, cb + nc * q / P, cb + nc * (q + 1) / P, P == 1 ? 1u : 0u});
+                    first.push_back(f);
+                }
+                split |= P > 1;
+            }
+        }
+        if (c->hist_bin && split) {
+            const uint32_t np = (uint32_t)first.size();
+            FK_TRY(ensure(c->hpieces, (uint64_t)np * 16));
+            FK_TRY(ensure(c->hpiece_first, (uint64_t)np * 4));
+            FK_TRY(ensure(c->hpiece_tot, ((uint64_t)np << F1) * 4));
+            HIP_TRY(hipMemcpyAsync(c->hpieces.p, pieces.data(), (uint64_t)np * 16, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(c->hpiece_first.p, first.data(), (uint64_t)np * 4, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
+            HIP_TRY(launch_expand_hist_pieces(c->KW, c->rsrc, c->chunks.as<Chunk>(), c->hpieces.as<uint4>(),
+                                              c->hpiece_first.as<uint32_t>(), np, k, F, F2,
+                                              c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(),
+                                              c->hpiece_tot.as<uint32_t>(), s));
+            HIP_TRY(hipStreamSynchronize(s));  // the host piece tables are released below
+        } else if (c->hist_bin) {
             HIP_TRY(launch_expand_hist_bin(c->KW, c->rsrc, c->chunks.as<Chunk>(), c->bin_chunk_begin.as<uint32_t>(),
                                            c->nlb, k, F, F2, c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
         } else {
@@ -1475,6 +1507,7 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)c->nlb + 1) * 4));
     if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), ((uint64_t)c->nlb + 1) * 4, hipMemcpyHostToDevice, s));
+    c->h_bcb = bcb;
     return FK_OK;
 }
 

@@ -154,6 +154,11 @@ hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chu
                                    int l1_threads = 0);
 hipError_t launch_expand_hist_sc(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
                                  int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);
+// pieces of bins (x = local bin, y / z = chunk range, w = whole bin): the same per piece, then the
+// earlier pieces' super-cell totals added (first_piece[i] = the bin's first piece)
+hipError_t launch_expand_hist_pieces(int KW, const uint64_t *rec, const Chunk *chunks, const uint4 *pieces,
+                                     const uint32_t *first_piece, uint32_t npieces, int k, int F, int F2,
+                                     uint64_t *cell_total, uint32_t *hist_sc, uint32_t *piece_tot, hipStream_t s);
 // one workgroup per local bin: cell totals and the per-chunk exclusive super-cell prefix in one pass
 hipError_t launch_expand_hist_bin(int KW, const uint64_t *rec, const Chunk *chunks, const uint32_t *bin_chunk_begin,
                                   uint32_t nlbins, int k, int F, int F2, uint64_t *cell_total, uint32_t *hist_sc,
