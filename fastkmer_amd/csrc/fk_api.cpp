@@ -253,6 +253,7 @@ struct fk_ctx {
     DevBuf records, counters, sig_status, sig_kmers;
     DevBuf tcnt;                  // fused map: records per tile (tiled record layout)
     DevBuf rec_hdr;               // fused map: every record's header word, in the record's tile slot
+    DevBuf tstat;                 // fused map: per tile (k-mers, positions)
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
@@ -475,7 +476,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
-                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr,
+                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->tstat,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
                       &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
@@ -563,7 +564,7 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
     const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
     if (end <= c->pm_tiles) return FK_OK;
-    if (c->tcnt.bytes < end * 4 || c->records.bytes < end * map_fused_tcap() * c->W * 8 ||
+    if (c->tcnt.bytes < end * 4 || c->tstat.bytes < end * 8 || c->records.bytes < end * map_fused_tcap() * c->W * 8 ||
         c->rec_hdr.bytes < end * map_fused_tcap() * 4)
         return set_err(FK_E_STATE, "streamed map: %llu tiles exceed the reserved record slots",
                        (unsigned long long)end);
@@ -571,7 +572,7 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
                              end - c->pm_tiles, c->fm, c->records.as<uint64_t>(), c->rec_hdr.as<uint32_t>(),
-                             c->tcnt.as<uint32_t>(),
+                             c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(),
                              c->counters.as<unsigned long long>(), s, c->fused_probe));
     c->pm_tiles = end;
     if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
@@ -617,6 +618,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         // record slots and per-tile counts of every tile this input can hold (kept on growth)
         const uint64_t tiles = (need + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
         if (c->tcnt.bytes < tiles * 4) FK_TRY(grow_keep(c->tcnt, tiles * 4, c->tcnt.bytes, s));
+        if (c->tstat.bytes < tiles * 8) FK_TRY(grow_keep(c->tstat, tiles * 8, c->tstat.bytes, s));
         const uint64_t rec_need = tiles * map_fused_tcap() * c->W * 8;
         if (c->records.bytes < rec_need) FK_TRY(grow_keep(c->records, rec_need, c->records.bytes, s));
         const uint64_t hdr_need = tiles * map_fused_tcap() * 4;
@@ -678,6 +680,7 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
         FK_TRY(ensure(c->records, tiles * map_fused_tcap() * c->W * 8));
         FK_TRY(ensure(c->rec_hdr, tiles * map_fused_tcap() * 4));
         FK_TRY(ensure(c->tcnt, tiles * 4));
+        FK_TRY(ensure(c->tstat, tiles * 8));
     }
     return FK_OK;
 }
@@ -747,6 +750,7 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     const uint64_t tile = fm_tile_bytes(c->fused_nt);
     const uint64_t ntiles = (n + tile - 1) / tile;
     FK_TRY(ensure(c->tcnt, ntiles * 4));
+    FK_TRY(ensure(c->tstat, ntiles * 8));
     FK_TRY(ensure(c->counters, 64));
     FK_TRY(ensure(c->records, ntiles * map_fused_tcap() * c->W * 8));
     FK_TRY(ensure(c->rec_hdr, ntiles * map_fused_tcap() * 4));
@@ -755,8 +759,10 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, c->fm,
                              c->records.as<uint64_t>(), c->rec_hdr.as<uint32_t>(), c->tcnt.as<uint32_t>(),
-                             c->counters.as<unsigned long long>(), s, c->fused_probe));
+                             c->tstat.as<uint32_t>(), c->counters.as<unsigned long long>(), s, c->fused_probe));
     HIP_TRY(hipEventRecord(c->ev[11], s));
+    HIP_TRY(launch_tile_totals(c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), ntiles,
+                               c->counters.as<unsigned long long>(), s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     uint64_t h[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
@@ -804,6 +810,8 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (c->pm_active && n) {
         // streamed map (fk_ingest launched the tiles as their bytes landed)
         if (!c->pm_last_seen) FK_TRY(premap_launch(c, n, true));  // the input ends here
+        HIP_TRY(launch_tile_totals(c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), c->pm_tiles,
+                                   c->counters.as<unsigned long long>(), s));
         uint64_t h[4] = {0, 0, 0, 0};
         HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

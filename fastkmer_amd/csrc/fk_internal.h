@@ -74,7 +74,10 @@ uint64_t fm_span_bytes(int nth);
 uint32_t map_fused_tcap();
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
                             uint64_t ntiles, FastMod fm, uint64_t *records, uint32_t *hdrs, uint32_t *tcnt,
-                            unsigned long long *counters, hipStream_t s, int probe = 0);
+                            uint32_t *tstat, unsigned long long *counters, hipStream_t s, int probe = 0);
+// counters[0] / [1] / [3] = records / k-mers / positions summed over the fused map's tiles [0, ntiles)
+hipError_t launch_tile_totals(const uint32_t *tcnt, const uint32_t *tstat, uint64_t ntiles,
+                              unsigned long long *counters, hipStream_t s);
 
 // ---- records to partition: dense (tcnt == null: nrec records, cut into PART_TILE tiles) or
 // tiled, as the fused map writes them (tile t holds tcnt[t] records at rec + t * tcap * W).
