@@ -120,6 +120,9 @@ def lib():
         "fk_map_bin_kmers": (ctypes.c_int, [P, P]),
         "fk_lpt_owners": (ctypes.c_int, [P, I32, I32, P]),
         "fk_set_bin_owners": (ctypes.c_int, [P, P, P]),
+        "fk_signature_slots": (U64, [P]),
+        "fk_signature_counts": (ctypes.c_int, [P, P, U64]),
+        "fk_write_bin_signatures": (ctypes.c_int, [P, P, U64, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -233,6 +236,7 @@ class KmerCounter:
         self.k, self.m, self.x, self.use_ht = k, m, x, bool(use_ht)
         self.n_ranks, self.rank = n_ranks, rank
         self._cfg = make_config(k, m, x, B, use_ht, sequence_type, False, n_ranks, rank, device)
+        self._device = device
         h = ctypes.c_void_p()
         _check(L.fk_create(ctypes.byref(self._cfg), ctypes.byref(h)))
         self._h = h
@@ -380,6 +384,29 @@ class KmerCounter:
     def write_bins(self, out_dir: str) -> None:
         _check(lib().fk_write_bins(self._h, out_dir.encode()))
 
+    # -- bin-signature diagnostics (executeFindBinSignaturesJob, SBKC:956-986)
+    def signature_counts(self, out=None):
+        """getBinSignatures (SBKC:772-917) over the ingested input: a device
+        int64 tensor of 4^m + 1 super-k-mer counts indexed by signature value
+        (``out``, if given, must hold that many).  The input stays ingested."""
+        import torch
+        n = lib().fk_signature_slots(self._h)
+        if out is None:
+            out = torch.empty(n, dtype=torch.int64, device=self._torch_device())
+        if out.numel() < n or out.dtype != torch.int64 or not out.is_cuda or not out.is_contiguous():
+            raise ValueError(f"signature counts need a contiguous device int64 tensor of {n} entries")
+        _check(lib().fk_signature_counts(self._h, ctypes.c_void_p(out.data_ptr()), out.numel()))
+        return out
+
+    def write_bin_signatures(self, counts, out_dir: str) -> None:
+        """saveBinSignatures (SBKC:920-953) for the bins this rank owns."""
+        _check(lib().fk_write_bin_signatures(self._h, ctypes.c_void_p(counts.data_ptr()), counts.numel(),
+                                             out_dir.encode()))
+
+    def _torch_device(self):
+        import torch
+        return torch.device("cuda", self._device if self._device >= 0 else torch.cuda.current_device())
+
     def stats(self) -> dict:
         st = fk_stats()
         _check(lib().fk_get_stats(self._h, ctypes.byref(st)))
@@ -411,3 +438,18 @@ def execute_job(configuration: TestConfiguration) -> KmerCounter:
     if configuration.write:
         kc.write_bins(configuration.outputDir)
     return kc
+
+
+def execute_find_bin_signatures_job(configuration: TestConfiguration):
+    """SparkBinKmerCounter.executeFindBinSignaturesJob (SBKC:956-986) on one GPU:
+    per-signature super-k-mer counts of the dataset, written as
+    ``configuration.outputDir/bin_signatures<b>.txt``.  Returns the counts (a
+    device int64 tensor indexed by signature value)."""
+    with open(configuration.dataset, "rb") as f:
+        data = f.read()
+    with KmerCounter(configuration.k, configuration.m, configuration.x, configuration.max_b,
+                     configuration.useHT, configuration.sequenceType) as kc:
+        kc.ingest(data)
+        counts = kc.signature_counts()
+        kc.write_bin_signatures(counts, configuration.outputDir)
+    return counts

@@ -1764,3 +1764,126 @@ FK_EXPORT int fk_write_bins(fk_ctx *c, const char *out_dir) {
         if (e) return set_err(FK_E_IO, "writing bin files under %s failed", out_dir);
     return FK_OK;
 }
+
+// ---------------------------------------------------------------------------
+// bin-signature diagnostics (executeFindBinSignaturesJob, SBKC:956-986)
+// ---------------------------------------------------------------------------
+
+FK_EXPORT uint64_t fk_signature_slots(const fk_ctx *c) { return c ? (1ull << (2 * c->cfg.m)) + 1ull : 0ull; }
+
+// getBinSignatures (SBKC:772-917) over the ingested input: the FASTA parse
+// (fk_parse.inc, look-back variant) and one pass of k_bin_signatures.  The
+// input stays as it was, so fk_map may follow.
+FK_EXPORT int fk_signature_counts(fk_ctx *c, void *d_counts, uint64_t n_counts) {
+    if (!c || !d_counts) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
+    const uint64_t slots = fk_signature_slots(c);
+    if (n_counts < slots)
+        return set_err(FK_E_RANGE, "signature counts hold %llu entries, need 4^m + 1 = %llu",
+                       (unsigned long long)n_counts, (unsigned long long)slots);
+    if (c->pm_active && !c->pm_last_seen)
+        return set_err(FK_E_STATE, "fk_signature_counts inside a streamed input: finish it with fk_ingest(..., last = 1)");
+    hipStream_t s = c->stream;
+    const uint64_t n = c->d_fasta ? c->n_fasta : 0;
+    HIP_TRY(hipMemsetAsync(d_counts, 0, slots * 8, s));
+    if (n) {
+        const uint64_t ntiles = (n + ENC_TILE - 1) / ENC_TILE;
+        const uint64_t code_words = n / 16 + 2 * POS_PAD_WORDS + 512;
+        const uint64_t valid_words = n / 32 + 2 * POS_PAD_WORDS + 512;
+        FK_TRY(ensure(c->tile_last_nl, ntiles * 8));
+        FK_TRY(ensure(c->tile_off, ntiles * 8));
+        FK_TRY(ensure(c->npos_dev, 16));
+        FK_TRY(ensure(c->codes, code_words * 4));
+        FK_TRY(ensure(c->valid, valid_words * 4));
+        HIP_TRY(hipMemsetAsync(c->codes.p, 0, code_words * 4, s));
+        HIP_TRY(hipMemsetAsync(c->valid.p, 0, valid_words * 4, s));
+        HIP_TRY(hipMemsetAsync(c->npos_dev.p, 0, 16, s));
+        HIP_TRY(hipMemsetAsync(c->tile_last_nl.p, 0, ntiles * 8, s));
+        HIP_TRY(hipMemsetAsync(c->tile_off.p, 0, ntiles * 8, s));
+        HIP_TRY(launch_fasta_parse(false, c->d_fasta, n, c->tile_last_nl.as<uint64_t>(), c->tile_off.as<uint64_t>(),
+                                   c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), c->npos_dev.as<uint64_t>(), s));
+        HIP_TRY(launch_bin_signatures(c->codes.as<uint32_t>(), c->valid.as<uint32_t>(), n, c->npos_dev.as<uint64_t>(),
+                                      c->cfg.k, c->cfg.m, (unsigned long long *)d_counts, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return FK_OK;
+}
+
+// longToString (PKG:616-634): always nucleotidesPerLong = 31 characters, the
+// signature's base-4 digits right-aligned behind 'A's (its length argument is unused).
+static void signature_string(uint64_t v, char out[31]) {
+    static const char rep[4] = {'A', 'C', 'G', 'T'};
+    for (int j = 30; j >= 0; --j) {
+        out[j] = rep[v & 3u];
+        v >>= 2;
+    }
+}
+
+// saveBinSignatures (SBKC:920-953): <out_dir>/bin_signatures<b>.txt for every
+// bin this rank owns that holds a signature, "<signature>\t<count>\n" lines
+// (ascending signature; the reference iterates a HashMap) and "Total\t<sum>\n".
+FK_EXPORT int fk_write_bin_signatures(fk_ctx *c, const void *d_counts, uint64_t n_counts, const char *out_dir) {
+    if (!c || !d_counts || !out_dir) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
+    const uint64_t slots = fk_signature_slots(c);
+    if (n_counts < slots)
+        return set_err(FK_E_RANGE, "signature counts hold %llu entries, need 4^m + 1 = %llu",
+                       (unsigned long long)n_counts, (unsigned long long)slots);
+    hipStream_t s = c->stream;
+    const unsigned long long *counts = (const unsigned long long *)d_counts;
+    DevBuf nz, pairs;
+    struct Free {
+        DevBuf *b[2];
+        ~Free() {
+            for (DevBuf *x : b) release(*x);
+        }
+    } guard{{&nz, &pairs}};
+    FK_TRY(ensure(nz, 8));
+    unsigned long long nnz = 0;
+    HIP_TRY(hipMemsetAsync(nz.p, 0, 8, s));
+    HIP_TRY(launch_sig_compact(counts, slots, nullptr, nz.as<unsigned long long>(), s));
+    HIP_TRY(hipMemcpyAsync(&nnz, nz.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint64_t> h(2 * nnz);
+    if (nnz) {
+        FK_TRY(ensure(pairs, nnz * 16));
+        HIP_TRY(hipMemsetAsync(nz.p, 0, 8, s));
+        HIP_TRY(launch_sig_compact(counts, slots, pairs.as<uint64_t>(), nz.as<unsigned long long>(), s));
+        HIP_TRY(hipMemcpyAsync(h.data(), pairs.p, nnz * 16, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    // (bin, signature) order; bins owned by other ranks are theirs to write
+    std::vector<std::pair<uint64_t, uint64_t>> rows;  // (bin << 32 | signature, count)
+    rows.reserve(nnz);
+    for (uint64_t i = 0; i < nnz; ++i) {
+        const uint32_t sig = (uint32_t)h[2 * i];
+        const int32_t b = (int32_t)bin_of_signature(sig, c->fm);
+        if (owns(c, b)) rows.emplace_back(((uint64_t)b << 32) | sig, h[2 * i + 1]);
+    }
+    std::sort(rows.begin(), rows.end());
+    if (rows.empty()) return FK_OK;
+    if (mkdir_p(out_dir) != 0) return set_err(FK_E_IO, "cannot create %s: %s", out_dir, strerror(errno));
+    const std::string dir(out_dir);
+    std::string text;
+    for (size_t i = 0; i < rows.size();) {
+        const uint32_t b = (uint32_t)(rows[i].first >> 32);
+        uint64_t tot = 0;
+        text.clear();
+        for (; i < rows.size() && (uint32_t)(rows[i].first >> 32) == b; ++i) {
+            char sig[31];
+            signature_string((uint32_t)rows[i].first, sig);
+            text.append(sig, 31);
+            text.push_back('\t');
+            text += std::to_string(rows[i].second);
+            text.push_back('\n');
+            tot += rows[i].second;
+        }
+        text += "Total\t" + std::to_string(tot) + "\n";
+        const std::string path = dir + "/bin_signatures" + std::to_string(b) + ".txt";
+        FILE *f = fopen(path.c_str(), "wb");
+        const bool ok = f && fwrite(text.data(), 1, text.size(), f) == text.size();
+        if (f && fclose(f) != 0) return set_err(FK_E_IO, "closing %s failed", path.c_str());
+        if (!ok) return set_err(FK_E_IO, "writing %s failed", path.c_str());
+    }
+    return FK_OK;
+}

@@ -63,6 +63,11 @@ hipError_t launch_superkmers(int W, const uint32_t *codes, const uint32_t *valid
                              const uint64_t *npos_dev, int k, int m, FastMod fm, uint64_t *records, uint64_t rec_cap,
                              uint64_t *status, uint64_t *tile_kmers, unsigned long long *counters, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, uint64_t n, uint64_t v, hipStream_t s);
+// ---- bin-signature diagnostics (fk_bin_signatures.inc, getBinSignatures SBKC:772-917)
+hipError_t launch_bin_signatures(const uint32_t *codes, const uint32_t *valid, uint64_t npos_bound,
+                                 const uint64_t *npos_dev, int k, int m, unsigned long long *counts, hipStream_t s);
+hipError_t launch_sig_compact(const unsigned long long *counts, uint64_t n, uint64_t *pairs, unsigned long long *nout,
+                              hipStream_t s);
 
 // ---- fused parse + signature (fk_map_fused.inc): FASTA bytes -> records in one kernel
 // for (k, m) with an instantiation; tiles of fm_tile_bytes(nth) FASTA bytes (nth = 256 or 512

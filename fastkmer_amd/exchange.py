@@ -269,3 +269,33 @@ def execute_job_distributed(configuration, group=None, device=None, rounds=None)
     if configuration.write:
         kc.write_bins(configuration.outputDir)
     return kc
+
+
+def execute_find_bin_signatures_job_distributed(configuration, group=None, device=None):
+    """executeFindBinSignaturesJob (SBKC:956-986) for one rank of a job.
+
+    Each rank counts the signatures of its shard (getBinSignatures, SBKC:772-917),
+    one all-reduce of the 4^m + 1 counts merges them (the reduceByKey of
+    SBKC:984), and each rank writes the ``bin_signatures<b>.txt`` of the bins it
+    owns.  A long sequence cut between ranks is cut there, as the reference's
+    input splits cut it.  Returns the merged counts (device tensor)."""
+    import fastkmer_amd as fk
+    from fastkmer_amd.sharding import read_shard
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    piece = read_shard(configuration.dataset, world, rank, configuration.k).piece
+    with fk.KmerCounter(configuration.k, configuration.m, configuration.x, configuration.max_b,
+                        configuration.useHT, configuration.sequenceType, n_ranks=world, rank=rank,
+                        device=dev.index if dev.index is not None else -1) as kc:
+        kc.ingest(piece)
+        counts = kc.signature_counts()
+        if dist.get_backend(group) == "gloo":
+            host = counts.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            counts.copy_(host)
+        else:
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        torch.cuda.synchronize(dev)
+        kc.write_bin_signatures(counts, configuration.outputDir)
+    return counts

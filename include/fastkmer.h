@@ -180,6 +180,21 @@ int fk_get_bin(fk_ctx *ctx, int32_t bin, uint64_t *keys, uint32_t *counts, size_
 int fk_write_bins(fk_ctx *ctx, const char *out_dir);
 int fk_get_stats(fk_ctx *ctx, fk_stats *out);
 
+/* ---- bin-signature diagnostics (executeFindBinSignaturesJob, SBKC:956-986) ----
+ * fk_signature_counts: after the final fk_ingest (the input is left in place,
+ *   fk_map may follow), d_counts[v] (device memory of the ctx device, uint64)
+ *   = super-k-mers with signature v over this rank's input -- getBinSignatures
+ *   (SBKC:772-917); v = 4^m when every m-mer of the window is forbidden.  It
+ *   needs fk_signature_slots(ctx) = 4^m + 1 entries.  Across ranks, sum the
+ *   arrays (an all-reduce: the reduceByKey of SBKC:984) before writing.
+ * fk_write_bin_signatures: saveBinSignatures (SBKC:920-953) for the bins this
+ *   rank owns: <out_dir>/bin_signatures<b>.txt, "<signature>\t<count>\n" lines
+ *   (longToString: 31 characters, PKG:616-634) in ascending signature order,
+ *   then "Total\t<sum>\n"; bins without signatures get no file. */
+uint64_t fk_signature_slots(const fk_ctx *ctx);
+int fk_signature_counts(fk_ctx *ctx, void *d_counts, uint64_t n_counts);
+int fk_write_bin_signatures(fk_ctx *ctx, const void *d_counts, uint64_t n_counts, const char *out_dir);
+
 #ifdef __cplusplus
 }
 #endif

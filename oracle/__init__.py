@@ -62,6 +62,11 @@ def lib():
                                      ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_int64]
         L.fko_trace_read.restype = ctypes.c_int64
+        L.fko_bin_signatures.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_void_p]
+        L.fko_bin_signatures.restype = ctypes.c_int
+        L.fko_write_bin_signatures.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]
+        L.fko_write_bin_signatures.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -163,3 +168,23 @@ def trace_read(read: bytes, k: int, m: int, B: int):
     if n < 0:
         raise ValueError("invalid parameters")
     return [(int(st[i]), int(ln[i]), int(bn[i])) for i in range(n)]
+
+
+def bin_signatures(fasta: bytes, k: int, m: int):
+    """getBinSignatures (SBKC:772-917) merged over reads: int64 counts[0..4^m],
+    super-k-mers per signature value (fko_bin_signatures)."""
+    import numpy as np
+    counts = np.zeros((1 << (2 * m)) + 1, dtype=np.int64)
+    if lib().fko_bin_signatures(fasta, len(fasta), k, m, counts.ctypes.data) != 0:
+        raise ValueError(f"invalid parameters k={k} m={m}")
+    return counts
+
+
+def write_bin_signatures(counts, m: int, B: int, out_dir: str) -> None:
+    """saveBinSignatures (SBKC:920-953) for every bin: bin_signatures<b>.txt."""
+    import numpy as np
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    if c.shape != ((1 << (2 * m)) + 1,):
+        raise ValueError("counts must hold 4^m + 1 entries")
+    if lib().fko_write_bin_signatures(c.ctypes.data, m, B, out_dir.encode()) != 0:
+        raise OSError(f"writing bin signatures under {out_dir} failed")

@@ -19,6 +19,8 @@
  *   - extractKXmersHT (hash count, no "EOF")     SparkBinKmerCounter.scala:664-739
  *   - TestConfiguration.b = min(4^m, B)          src/main/scala/skc/test/package.scala:32
  *   - read = record value with '\n' removed      SparkBinKmerCounter.scala:62-65
+ *   - getBinSignatures / saveBinSignatures       SparkBinKmerCounter.scala:772-953
+ *     (bin-signature diagnostics), longToString  package.scala:616-634
  *
  * Control flow of the map side (getSuperKmers) is kept step for step,
  * including the O(k) invalid-byte scan per window, the O(k) signature
@@ -610,4 +612,126 @@ FKO_API int64_t fko_trace_read(const uint8_t *read, int64_t n, int32_t k, int32_
     for (int32_t b = 0; b < p.B; ++b) free(r.bins[b].keys);
     free(r.bins);
     return r.superkmers;
+}
+
+/* ------------------------------------------------------------------ */
+/* bin-signature diagnostics: executeFindBinSignaturesJob               */
+/* (SparkBinKmerCounter.scala:956-986)                                  */
+/* ------------------------------------------------------------------ */
+
+/* getBinSignatures (SBKC:772-917) for one read: the getSuperKmers walk
+ * (same N jumps, expiry test and strict "<"), but each super-k-mer adds 1 to
+ * counts[signature] (the out(bin) HashMap update of :828-830, :844-846,
+ * :868-870, :890-899) instead of emitting k-mers.  The bin and the
+ * signature string are functions of the value, applied by the writer. */
+static void bin_signatures_read(int64_t *counts, const fko_params *p, const uint8_t *cur, int64_t n) {
+    const int k = p->k, m = p->m;
+    if (n < k) return; /* :810 */
+    int32_t min_value = -1;
+    int64_t min_pos = -1; /* Signature(-1,-1), :812 */
+    int64_t sk_start = 0, i = 0, nf, nl;
+    while (i < n - k + 1) {                           /* :818 */
+        first_last_invalid(cur, i, i + k, &nf, &nl); /* :820 */
+        if (nf != -1) {
+            if (sk_start < i) counts[min_value]++; /* :826-830 */
+            sk_start = i + nl + 1;                  /* :835 */
+            i += nl + 1;                            /* :836 */
+        } else {
+            if (i > min_pos) { /* :842 */
+                if (sk_start < i) {
+                    counts[min_value]++; /* :843-846 */
+                    sk_start = i;
+                }
+                int32_t rel;
+                min_value = get_signature(p, cur, i, &rel); /* :854 */
+                min_pos = rel + i;
+            } else {
+                int32_t last = norm_of(p, mmer_at(cur, i + k - m, m)); /* :861 */
+                if (last < min_value) {                                 /* :863 */
+                    if (sk_start < i) {
+                        counts[min_value]++; /* :866-870 */
+                        sk_start = i;
+                    }
+                    min_value = last; /* :876 */
+                    min_pos = i + k - m;
+                }
+            }
+            i += 1;
+        }
+    }
+    if (n - sk_start >= k) { /* :886 */
+        first_last_invalid(cur, i, n, &nf, &nl);
+        if (nf == -1 || i + nf >= sk_start + k) counts[min_value]++; /* :892-902 */
+    }
+}
+
+typedef struct {
+    int64_t *counts;
+    fko_params *p;
+} sig_ctx;
+
+static void sig_read(void *vctx, const uint8_t *read, int64_t n) {
+    sig_ctx *c = (sig_ctx *)vctx;
+    bin_signatures_read(c->counts, c->p, read, n);
+}
+
+/* counts[0 .. 4^m] (zeroed here): super-k-mers per signature value over all
+ * reads of the FASTA, i.e. the per-bin HashMaps of getBinSignatures merged by
+ * the reduceByKey of SBKC:984.  Returns 0, or -1 on invalid parameters. */
+FKO_API int fko_bin_signatures(const uint8_t *fasta, size_t n, int32_t k, int32_t m, int64_t *counts) {
+    if (k < 1 || k > 64 || m < 1 || m > 15 || m > k || !counts) return -1;
+    fko_params p;
+    p.k = k;
+    p.m = m;
+    p.B = 1;
+    p.norm = NULL;
+    memset(counts, 0, (((size_t)1 << (2 * m)) + 1) * sizeof(int64_t));
+    sig_ctx c = {counts, &p};
+    for_each_read(fasta, n, sig_read, &c);
+    return 0;
+}
+
+/* saveBinSignatures (SBKC:920-953) for every bin with a signature:
+ * <dir>/bin_signatures<b>.txt, "<longToString(v)>\t<count>\n" per signature
+ * (longToString, PKG:616-634: 31 characters whatever m) and "Total\t<sum>\n".
+ * The reference iterates an immutable HashMap (order unspecified); lines are
+ * written in ascending signature value.  B is the requested bin count. */
+FKO_API int fko_write_bin_signatures(const int64_t *counts, int32_t m, int32_t B, const char *dir) {
+    if (m < 1 || m > 15 || B < 1) return -1;
+    if (mkdir(dir, 0755) != 0 && errno != EEXIST) return -1;
+    const int32_t nb = fko_clamp_bins(m, B);
+    const int64_t slots = ((int64_t)1 << (2 * m)) + 1;
+    /* signatures grouped by bin(min_s.value) (:777), ascending inside a bin */
+    int64_t *start = (int64_t *)calloc((size_t)nb + 1, sizeof(int64_t));
+    int64_t nz = 0;
+    for (int64_t v = 0; v < slots; ++v)
+        if (counts[v]) { start[fko_hash_to_bucket((int32_t)v, nb) + 1]++; ++nz; }
+    for (int32_t b = 0; b < nb; ++b) start[b + 1] += start[b];
+    int64_t *order = (int64_t *)malloc((size_t)(nz ? nz : 1) * sizeof(int64_t));
+    int64_t *fill = (int64_t *)malloc((size_t)nb * sizeof(int64_t));
+    memcpy(fill, start, (size_t)nb * sizeof(int64_t));
+    for (int64_t v = 0; v < slots; ++v)
+        if (counts[v]) order[fill[fko_hash_to_bucket((int32_t)v, nb)]++] = v;
+    char path[4096], sig[32];
+    int rc = 0;
+    for (int32_t b = 0; b < nb && rc == 0; ++b) {
+        if (start[b] == start[b + 1]) continue; /* out.filter(map.nonEmpty), :916 */
+        snprintf(path, sizeof(path), "%s/bin_signatures%d.txt", dir, b);
+        FILE *f = fopen(path, "wb");
+        if (!f) { rc = -2; break; }
+        int64_t tot = 0;
+        for (int64_t e = start[b]; e < start[b + 1]; ++e) {
+            int64_t x = order[e];
+            for (int j = 30; j >= 0; --j) { sig[j] = "ACGT"[x & 3]; x >>= 2; }
+            sig[31] = 0;
+            fprintf(f, "%s\t%lld\n", sig, (long long)counts[order[e]]);
+            tot += counts[order[e]];
+        }
+        fprintf(f, "Total\t%lld\n", (long long)tot);
+        fclose(f);
+    }
+    free(start);
+    free(order);
+    free(fill);
+    return rc;
 }

@@ -24,6 +24,8 @@ Followed (paths relative to /root/reference/src/main/scala/skc/):
   SparkBinKmerCounter.scala:34-169   getSuperKmers
   SparkBinKmerCounter.scala:428-660  extractKXmers
   SparkBinKmerCounter.scala:664-739  extractKXmersHT
+  SparkBinKmerCounter.scala:772-953  getBinSignatures, saveBinSignatures
+  package.scala:616-634  longToString
 """
 from __future__ import annotations
 
@@ -378,6 +380,65 @@ def get_super_kmers(k: int, m: int, b: int, reads: list[bytes], trace: list | No
                 elif i + nf >= sk_start + k:
                     emit(min_value, Kmer.from_bytes(i + nf, cur, sk_start))
     return out
+
+
+def long_to_string(num: int, length: int = 7) -> str:  # package.scala:616-634 (length unused)
+    result = [""] * NPL
+    cur = _jl(num)
+    for j in range(NPL - 1, -1, -1):
+        result[j] = "ACGT"[cur & 3]
+        cur = _shr(cur, 2)
+    return "".join(result)
+
+
+def get_bin_signatures(k: int, m: int, b: int, reads: list[bytes]) -> dict[int, dict[str, int]]:
+    """SparkBinKmerCounter.scala:772-917 (the HashMaps of bins with a signature)."""
+    out: dict[int, dict[str, int]] = {}
+    norm = fill_norm(m)
+    last_m_mask = _ji((1 << m * 2) - 1)
+
+    def update(sig_value):  # :828-830 (and the three copies below)
+        d = out.setdefault(hash_to_bucket(sig_value, b), {})
+        sig = long_to_string(sig_value, m)
+        d[sig] = d.get(sig, 0) + 1
+
+    for cur in reads:
+        if len(cur) >= k:
+            min_value, min_pos = -1, -1
+            sk_start, i = 0, 0
+            while i < len(cur) - k + 1:
+                nf, nl = first_and_last_invalid(cur, i, i + k)
+                if nf != -1:
+                    if sk_start < i:
+                        update(min_value)
+                    sk_start = i + nl + 1
+                    i += nl + 1
+                else:
+                    s = Kmer.from_bytes(k, cur, i)
+                    if i > min_pos:
+                        if sk_start < i:
+                            update(min_value)
+                            sk_start = i
+                        sv, sp = s.get_signature(m, norm)
+                        min_value, min_pos = sv, sp + i
+                    else:
+                        last = s.last_m(last_m_mask, norm, m)
+                        if last < min_value:
+                            if sk_start < i:
+                                update(min_value)
+                                sk_start = i
+                            min_value, min_pos = last, i + k - m
+                    i += 1
+            if len(cur) - sk_start >= k:
+                nf, nl = first_and_last_invalid(cur, i, len(cur))
+                if nf == -1 or i + nf >= sk_start + k:
+                    update(min_value)
+    return out
+
+
+def save_bin_signatures_text(sigs: dict[str, int]) -> str:  # SparkBinKmerCounter.scala:920-953
+    """One bin's file; lines in the dict's order (the reference's HashMap order)."""
+    return "".join(f"{s}\t{c}\n" for s, c in sigs.items()) + f"Total\t{sum(sigs.values())}\n"
 
 
 class RIndex:  # package.scala:562-601

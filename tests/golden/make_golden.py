@@ -8,6 +8,11 @@ transliteration (oracle/literal_ref.py) and the independent naive counter
 (tests/naive_oracle.py) produce the same files -- the reference itself cannot
 run here (no JVM/Spark/FASTdoop), see DESIGN.md "Oracle".
 
+<name>.binsig.json holds the bin-signature diagnostics of the same input
+({"bin_signatures<b>.txt": file text}, SparkBinKmerCounter.scala:772-953, lines
+in ascending signature order), written by the C oracle only when the literal
+transliteration of getBinSignatures gives the same (bin, signature, count) sets.
+
 Usage: python tests/golden/make_golden.py
 """
 from __future__ import annotations
@@ -84,6 +89,23 @@ def expected_files(fasta, k, m, x, B, sequence_type=0):
     return files, r
 
 
+def expected_binsig(fasta, k, m, B):
+    import tempfile
+    counts = oracle.bin_signatures(fasta, k, m)
+    with tempfile.TemporaryDirectory() as d:
+        oracle.write_bin_signatures(counts, m, B, d)
+        files = {}
+        for name in sorted(os.listdir(d)):
+            with open(os.path.join(d, name)) as f:
+                files[name] = f.read()
+    lit = literal_ref.get_bin_signatures(k, m, oracle.clamp_bins(m, B), literal_ref.parse_reads(fasta))
+    lit_files = {f"bin_signatures{b}.txt": literal_ref.save_bin_signatures_text(dict(sorted(d.items())))
+                 for b, d in lit.items()}
+    if lit_files != files:
+        raise SystemExit("literal getBinSignatures disagrees with the C oracle")
+    return files
+
+
 def main():
     index = {}
     for name, params, fasta in cases():
@@ -92,6 +114,8 @@ def main():
             f.write(fasta)
         with open(os.path.join(HERE, name + ".expected.json"), "w") as f:
             json.dump(files, f, indent=0, sort_keys=True)
+        with open(os.path.join(HERE, name + ".binsig.json"), "w") as f:
+            json.dump(expected_binsig(fasta, params["k"], params["m"], params["B"]), f, indent=0, sort_keys=True)
         index[name] = dict(params, total_kmers=r.total_kmers, distinct=r.distinct, nonempty_bins=len(files))
         print(f"{name}: {len(fasta)} B, {r.total_kmers} k-mers, {r.distinct} distinct, {len(files)} bins")
     with open(os.path.join(HERE, "index.json"), "w") as f:

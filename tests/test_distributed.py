@@ -225,6 +225,35 @@ def test_execute_job_distributed_rccl(tmp_path, use_ht, rounds):
             assert got[name] == want[name]
 
 
+def _binsig_worker(rank, world, port, cfg_kw):
+    _init(rank, world, port, "gloo")
+    try:
+        from fastkmer_amd.exchange import execute_find_bin_signatures_job_distributed
+        torch.cuda.set_device(0)
+        execute_find_bin_signatures_job_distributed(fk.TestConfiguration(**cfg_kw), device=torch.device("cuda", 0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_find_bin_signatures_job_distributed(tmp_path, world):
+    """executeFindBinSignaturesJob (SBKC:956-986) over `world` ranks sharing one GPU:
+    per-shard getBinSignatures, one all-reduce (the reduceByKey of :984), each rank
+    writes its bins' bin_signatures<b>.txt; the union equals the oracle's files."""
+    k, m, B = 28, 10, 2048
+    data = fk.synth_fasta(20_000, 100, 200_000, seed=31)
+    path = tmp_path / "in.fa"
+    path.write_bytes(data)
+    cfg = dict(dataset=str(path), outputDirectory=str(tmp_path / "out") + "/", k=k, m=m, x=3, max_b=B)
+    mp.spawn(_binsig_worker, args=(world, _free_port(), cfg), nprocs=world, join=True)
+    got = _read_bins(fk.TestConfiguration(**cfg).outputDir)
+    ref_dir = tmp_path / "ref"
+    oracle.write_bin_signatures(oracle.bin_signatures(data, k, m), m, B, str(ref_dir))
+    want = _read_bins(str(ref_dir))
+    assert len(want) > 100 and got == want
+
+
 # ---------------------------------------------------------------- per-rank file reads (CPU)
 
 def _fasta_variants():

@@ -164,3 +164,58 @@ def test_oracle_threads_match_single(threads):
             b = oracle.OracleResult(fa, k, m, B, threads=threads)
             assert (a.total_kmers, a.superkmers, a.reads, a.distinct) == (b.total_kmers, b.superkmers, b.reads, b.distinct)
             assert a.all_dict() == b.all_dict()
+
+
+# ---------------------------------------------------------------- bin-signature diagnostics
+
+def _binsig_files(counts, m, B, tmp_path):
+    d = tmp_path / f"sig_{m}_{B}"
+    d.parent.mkdir(parents=True, exist_ok=True)
+    oracle.write_bin_signatures(counts, m, B, str(d))
+    return {p.name: p.read_text() for p in d.iterdir()}
+
+
+def test_long_to_string_is_31_characters():
+    # longToString ignores its length argument (package.scala:616-634)
+    assert literal_ref.long_to_string(0, 10) == "A" * 31
+    assert literal_ref.long_to_string(enc("ACGTACGTAC"), 10) == "A" * 21 + "ACGTACGTAC"
+    assert literal_ref.long_to_string(4 ** 10, 10) == "A" * 20 + "C" + "A" * 10
+
+
+def test_bin_signatures_match_literal_random(tmp_path):
+    rng = random.Random(4321)
+    for trial in range(14):
+        k = rng.choice([5, 12, 21, 28, 31, 33, 55, 64])
+        m = min(k, rng.choice([1, 2, 3, 7, 10]))
+        B = rng.choice([1, 7, 64, 2048])
+        reads = []
+        for i in range(rng.randint(1, 6)):
+            alpha = rng.choice(["ACGT", "ACGTN", "AAAC", "ACGTT"])
+            reads.append(f">r{i}\n" + "".join(rng.choice(alpha) for _ in range(rng.randint(0, 150))) + "\n")
+        fa = "".join(reads).encode()
+        counts = oracle.bin_signatures(fa, k, m)
+        bc = oracle.clamp_bins(m, B)
+        lit = literal_ref.get_bin_signatures(k, m, bc, literal_ref.parse_reads(fa))
+        want = {f"bin_signatures{b}.txt": literal_ref.save_bin_signatures_text(dict(sorted(d.items())))
+                for b, d in lit.items()}
+        assert _binsig_files(counts, m, B, tmp_path / str(trial)) == want
+        # one count per super-k-mer of getSuperKmers (the same walk, SBKC:59-161)
+        assert int(counts.sum()) == oracle.OracleResult(fa, k, m, B).superkmers
+
+
+@pytest.mark.parametrize("name", sorted(golden_cases()))
+def test_bin_signatures_golden_fixture(name, tmp_path):
+    params = golden_cases()[name]
+    with open(os.path.join(GOLDEN, name + ".fa"), "rb") as f:
+        fasta = f.read()
+    with open(os.path.join(GOLDEN, name + ".binsig.json")) as f:
+        expected = json.load(f)
+    counts = oracle.bin_signatures(fasta, params["k"], params["m"])
+    assert _binsig_files(counts, params["m"], params["B"], tmp_path) == expected
+
+
+def test_bin_signatures_rejects_invalid_params():
+    with pytest.raises(ValueError):
+        oracle.bin_signatures(b">a\nACGT\n", 70, 10)
+    with pytest.raises(ValueError):
+        oracle.bin_signatures(b">a\nACGT\n", 8, 9)
