@@ -277,14 +277,20 @@ def execute_find_bin_signatures_job_distributed(configuration, group=None, devic
     Each rank counts the signatures of its shard (getBinSignatures, SBKC:772-917),
     one all-reduce of the 4^m + 1 counts merges them (the reduceByKey of
     SBKC:984), and each rank writes the ``bin_signatures<b>.txt`` of the bins it
-    owns.  A long sequence cut between ranks is cut there, as the reference's
-    input splits cut it.  Returns the merged counts (device tensor)."""
+    owns.  Short reads (sequenceType 0) are dealt as whole records
+    (sharding.read_record_shard), so the merged counts are the whole file's; a
+    long sequence (sequenceType 1) is cut between ranks with the k - 1 overlap
+    (sharding.read_shard), and a super-k-mer over a cut counts once per side, as
+    over the reference's input splits.  Returns the merged counts (device tensor)."""
     import fastkmer_amd as fk
-    from fastkmer_amd.sharding import read_shard
+    from fastkmer_amd.sharding import read_record_shard, read_shard
 
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    piece = read_shard(configuration.dataset, world, rank, configuration.k).piece
+    if configuration.sequenceType == 0:
+        piece = read_record_shard(configuration.dataset, world, rank)
+    else:
+        piece = read_shard(configuration.dataset, world, rank, configuration.k).piece
     with fk.KmerCounter(configuration.k, configuration.m, configuration.x, configuration.max_b,
                         configuration.useHT, configuration.sequenceType, n_ranks=world, rank=rank,
                         device=dev.index if dev.index is not None else -1) as kc:

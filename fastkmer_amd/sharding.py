@@ -201,3 +201,33 @@ def read_shard(path: str, world: int, rank: int, k: int, window: int = 4096) -> 
             q += len(chunk)
         piece = b">s\n" + body + bytes(ext) + b"\n"
         return ShardRead(piece, touched, lo, hi)
+
+
+def read_record_shard(path: str, world: int, rank: int, window: int = 1 << 16) -> bytes:
+    """Rank ``rank`` of ``world``'s whole records of the FASTA file ``path``
+    (positioned reads of its byte range only): the range [r*size/world,
+    (r+1)*size/world) moved forward to record starts (a '>' at a line start),
+    so every record is read by exactly one rank, as the short-read input format
+    hands whole records to one map task.  Rank 0 also gets any text before the
+    first header (which the parse ignores)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of {world}")
+    n = os.path.getsize(path)
+    with open(path, "rb") as f:
+        fd = f.fileno()
+
+        def start_at(p: int) -> int:
+            if p <= 0:
+                return 0
+            q = p - 1
+            while q < n:
+                buf = os.pread(fd, window + 1, q)
+                j = buf.find(b"\n>")
+                if j >= 0:
+                    return q + j + 1
+                q += window
+            return n
+
+        lo = start_at(rank * n // world)
+        hi = start_at((rank + 1) * n // world) if rank + 1 < world else n
+        return os.pread(fd, max(0, hi - lo), lo) if hi > lo else b""

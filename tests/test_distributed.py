@@ -225,6 +225,23 @@ def test_execute_job_distributed_rccl(tmp_path, use_ht, rounds):
             assert got[name] == want[name]
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 7, 50])
+def test_record_shards_hold_whole_records(tmp_path, world):
+    """sharding.read_record_shard: the ranks' pieces concatenate to the file and
+    each holds whole records, so per-rank signature counts add up exactly."""
+    from fastkmer_amd.sharding import read_record_shard
+    rng = random.Random(world)
+    data = b"junk\n" + b"".join(b">r%d\n" % i + bytes(rng.choice(b"ACGTN") for _ in range(rng.randint(0, 300))) + b"\n"
+                                for i in range(200))
+    path = tmp_path / "in.fa"
+    path.write_bytes(data)
+    pieces = [read_record_shard(str(path), world, r, window=64) for r in range(world)]
+    assert b"".join(pieces) == data
+    assert all(p[:1] == b">" for p in pieces[1:] if p)
+    total = sum(oracle.bin_signatures(p, 21, 7) for p in pieces)
+    assert (total == oracle.bin_signatures(data, 21, 7)).all()
+
+
 def _binsig_worker(rank, world, port, cfg_kw):
     _init(rank, world, port, "gloo")
     try:
