@@ -123,6 +123,7 @@ def lib():
         "fk_signature_slots": (U64, [P]),
         "fk_signature_counts": (ctypes.c_int, [P, P, U64]),
         "fk_write_bin_signatures": (ctypes.c_int, [P, P, U64, ctypes.c_char_p]),
+        "fk_find_bin_signatures": (ctypes.c_int, [P, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1887,3 +1887,19 @@ FK_EXPORT int fk_write_bin_signatures(fk_ctx *c, const void *d_counts, uint64_t 
     }
     return FK_OK;
 }
+
+// executeFindBinSignaturesJob (SBKC:956-986) for one rank holding the whole
+// input: fk_signature_counts into a context-owned buffer, then the writer.
+FK_EXPORT int fk_find_bin_signatures(fk_ctx *c, const char *out_dir) {
+    if (!c || !out_dir) return set_err(FK_E_INVALID, "null argument");
+    DeviceGuard dg_(c->device);
+    const uint64_t slots = fk_signature_slots(c);
+    DevBuf counts;
+    struct Free {
+        DevBuf *b;
+        ~Free() { release(*b); }
+    } guard{&counts};
+    FK_TRY(ensure(counts, slots * 8));
+    FK_TRY(fk_signature_counts(c, counts.p, slots));
+    return fk_write_bin_signatures(c, counts.p, slots, out_dir);
+}

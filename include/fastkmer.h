@@ -194,6 +194,9 @@ int fk_get_stats(fk_ctx *ctx, fk_stats *out);
 uint64_t fk_signature_slots(const fk_ctx *ctx);
 int fk_signature_counts(fk_ctx *ctx, void *d_counts, uint64_t n_counts);
 int fk_write_bin_signatures(fk_ctx *ctx, const void *d_counts, uint64_t n_counts, const char *out_dir);
+/* The whole job on one rank (n_ranks == 1, or each rank's own input unmerged):
+ * fk_signature_counts into a library-owned buffer, then fk_write_bin_signatures. */
+int fk_find_bin_signatures(fk_ctx *ctx, const char *out_dir);
 
 #ifdef __cplusplus
 }

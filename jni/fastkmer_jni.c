@@ -101,6 +101,18 @@ JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_writeBins(JNIEnv *en
     if (rc != FK_OK) throw_fk(env, rc);
 }
 
+/* def findBinSignatures(h, outDir): Unit -- executeFindBinSignaturesJob's
+ * bin_signatures<b>.txt files (SBKC:956-986) for this context's input */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_findBinSignatures(JNIEnv *env, jobject self, jlong h,
+                                                                             jstring dir) {
+    (void)self;
+    const char *d = (*env)->GetStringUTFChars(env, dir, NULL);
+    if (!d) return;
+    const int rc = fk_find_bin_signatures(ctx_of(h), d);
+    (*env)->ReleaseStringUTFChars(env, dir, d);
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
 /* def destroy(h): Unit */
 JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_destroy(JNIEnv *env, jobject self, jlong h) {
     (void)env;

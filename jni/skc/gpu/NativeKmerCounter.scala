@@ -25,26 +25,42 @@ object NativeKmerCounter {
   @native def finish(h: Long): Unit
   @native def binSizes(h: Long): Array[Long]
   @native def writeBins(h: Long, outDir: String): Unit
+  @native def findBinSignatures(h: Long, outDir: String): Unit
   @native def destroy(h: Long): Unit
 
   /** The file is streamed in mapped windows of `window` bytes (fk_ingest appends them). */
+  private def ingestFile(h: Long, dataset: String, window: Long): Unit = {
+    val ch = FileChannel.open(Paths.get(dataset), StandardOpenOption.READ)
+    try {
+      val size = ch.size()
+      if (size == 0L) ingest(h, java.nio.ByteBuffer.allocateDirect(0), 0L, true)
+      var off = 0L
+      while (off < size) {
+        val len = math.min(window, size - off)
+        ingest(h, ch.map(FileChannel.MapMode.READ_ONLY, off, len), len, off + len >= size)
+        off += len
+      }
+    } finally ch.close()
+  }
+
   def executeJob(configuration: TestConfiguration, device: Int = -1, window: Long = 1L << 30): Unit = {
     val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
       configuration.useHT, configuration.sequenceType, 1, 0, device)
     try {
-      val ch = FileChannel.open(Paths.get(configuration.dataset), StandardOpenOption.READ)
-      try {
-        val size = ch.size()
-        if (size == 0L) ingest(h, java.nio.ByteBuffer.allocateDirect(0), 0L, true)
-        var off = 0L
-        while (off < size) {
-          val len = math.min(window, size - off)
-          ingest(h, ch.map(FileChannel.MapMode.READ_ONLY, off, len), len, off + len >= size)
-          off += len
-        }
-      } finally ch.close()
+      ingestFile(h, configuration.dataset, window)
       finish(h)
       if (configuration.write) writeBins(h, configuration.outputDir)
+    } finally destroy(h)
+  }
+
+  /** SparkBinKmerCounter.executeFindBinSignaturesJob (:956-986): bin_signatures<b>.txt. */
+  def executeFindBinSignaturesJob(configuration: TestConfiguration, device: Int = -1,
+                                  window: Long = 1L << 30): Unit = {
+    val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
+      configuration.useHT, configuration.sequenceType, 1, 0, device)
+    try {
+      ingestFile(h, configuration.dataset, window)
+      findBinSignatures(h, configuration.outputDir)
     } finally destroy(h)
   }
 }

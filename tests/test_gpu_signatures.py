@@ -183,3 +183,15 @@ def test_execute_find_bin_signatures_job(tmp_path):
     want = _oracle_files(oracle.bin_signatures(fasta, k, m), m, B, tmp_path / "ref")
     assert _files(cfg.outputDir) == want and len(want) == 64
     assert int(counts.sum()) == oracle.OracleResult(fasta, k, m, B).superkmers
+
+
+def test_find_bin_signatures_one_call(tmp_path):
+    """fk_find_bin_signatures (the JNI shim's findBinSignatures): counts into a
+    library-owned buffer and writes the same files."""
+    k, m, B = 28, 10, 2048
+    fasta = fk.synth_fasta(8_000, 100, 100_000, seed=13)
+    with fk.KmerCounter(k, m, 3, B) as kc:
+        kc.ingest(fasta)
+        assert fk.lib().fk_find_bin_signatures(kc._h, str(tmp_path / "gpu").encode()) == 0
+    want = _oracle_files(oracle.bin_signatures(fasta, k, m), m, B, tmp_path / "ref")
+    assert _files(str(tmp_path / "gpu")) == want
