@@ -214,6 +214,7 @@ struct fk_ctx {
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
     uint32_t greedy_cap = 0;   // FASTKMER_GREEDY_CAP (probe): pack cells into buckets of up to this many keys (0 = wave_cap)
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
+    uint32_t wave_slots = 768;  // FASTKMER_WAVE_SLOTS: table slots of a 512-key wave bucket (768 or 1024)
     int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
@@ -408,6 +409,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (el && el[0]) c->expand_levels = atoi(el);
     const char *wc = getenv("FASTKMER_WAVE_CAP");
     if (wc && wc[0]) c->wave_cap = (uint32_t)atoi(wc);
+    if (const char *ws = getenv("FASTKMER_WAVE_SLOTS"); ws && ws[0]) c->wave_slots = (uint32_t)atoi(ws);
     if (const char *gc = getenv("FASTKMER_GREEDY_CAP"); gc && gc[0]) c->greedy_cap = (uint32_t)atoi(gc);
     const char *f2 = getenv("FASTKMER_F2");
     if (const char *hb = getenv("FASTKMER_HIST_BIN"); hb && hb[0]) c->hist_bin = atoi(hb);
@@ -1201,7 +1203,8 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
                                                c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                               c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, nullptr, s));
+                                               c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
+                                               nullptr, s));
         else
             HIP_TRY(launch_bucket_count128_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
                                                 c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),

@@ -177,7 +177,7 @@ hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave
                                uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts, hipStream_t s);
 hipError_t launch_bucket_count64_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique, int bpw,
-                                      uint32_t wave_cap, const uint32_t *list, hipStream_t s);
+                                      uint32_t wave_cap, uint32_t wave_slots, const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, const uint32_t *list, hipStream_t s);

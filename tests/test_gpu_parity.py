@@ -418,6 +418,19 @@ def test_big_bins_two_level_vs_oracle():
     assert_same_as_oracle(kc, ref)
 
 
+@pytest.mark.parametrize("slots", ["768", "1024"])
+def test_wave_tables_of_distinct_keys_vs_oracle(monkeypatch, slots):
+    # reads of a 3 Gbp virtual genome: nearly every k-mer is distinct, so the
+    # 512-key wave buckets fill their tables with ~512 distinct keys (2/3 of
+    # the 768 slots: the longest probe runs)
+    monkeypatch.setenv("FASTKMER_WAVE_SLOTS", slots)
+    fasta = fk.synth_fasta(100_000, 100, 3_000_000_000, seed=61)
+    kc = run_counter(fasta, 28, 10, 3, 64)
+    ref = oracle.OracleResult(fasta, 28, 10, 64)
+    assert kc.stats()["distinct"] > 0.95 * ref.total_kmers
+    assert_same_as_oracle(kc, ref)
+
+
 @pytest.mark.parametrize("env", [
     {"FASTKMER_COUNT_MODE": "0"},                                   # one workgroup per <= 2048-key bucket
     {"FASTKMER_EXPAND_LEVELS": "1"},                                # one-level write-combined scatter
@@ -425,6 +438,7 @@ def test_big_bins_two_level_vs_oracle():
     {"FASTKMER_WAVE_CAP": "256", "FASTKMER_WAVE_BPW": "1"},
     {"FASTKMER_WAVE_CAP": "128", "FASTKMER_WAVE_BPW": "2", "FASTKMER_DEBUG_CELL_TARGET": "64"},
     {"FASTKMER_X2_L1": "1024"},                                      # 1024-record level-1 batches
+    {"FASTKMER_WAVE_SLOTS": "1024"},                                 # 2 slots per key in the wave tables
 ])
 def test_count_variants_identical(monkeypatch, env):
     # every count-stage variant gives the default path's result, bit for bit
