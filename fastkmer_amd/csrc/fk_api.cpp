@@ -214,7 +214,8 @@ struct fk_ctx {
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
     uint32_t greedy_cap = 0;   // FASTKMER_GREEDY_CAP (probe): pack cells into buckets of up to this many keys (0 = wave_cap)
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
-    uint32_t wave_slots = 768;  // FASTKMER_WAVE_SLOTS: table slots of a 512-key wave bucket (768 or 1024)
+    uint32_t wave_slots = 768;  // FASTKMER_WAVE_SLOTS: table slots of a 512-key wave bucket (768 or 1024;
+                                // 128-bit keys: 384 or 512 per 256-key bucket alike)
     int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
     int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
@@ -1208,7 +1209,8 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         else
             HIP_TRY(launch_bucket_count128_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
                                                 c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                                c->bucket_unique.as<uint64_t>(), s));
+                                                c->bucket_unique.as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
+                                                s));
         uint32_t ntier[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

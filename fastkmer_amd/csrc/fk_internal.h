@@ -155,7 +155,7 @@ constexpr uint32_t WAVE_BUCKET_CAP = 512;
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                                       hipStream_t s);
+                                       bool small_tables, hipStream_t s);
 hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
                                    uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
                                    const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s,

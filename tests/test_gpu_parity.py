@@ -419,14 +419,16 @@ def test_big_bins_two_level_vs_oracle():
 
 
 @pytest.mark.parametrize("slots", ["768", "1024"])
-def test_wave_tables_of_distinct_keys_vs_oracle(monkeypatch, slots):
+@pytest.mark.parametrize("k,m", [(28, 10), (55, 12)])
+def test_wave_tables_of_distinct_keys_vs_oracle(monkeypatch, slots, k, m):
     # reads of a 3 Gbp virtual genome: nearly every k-mer is distinct, so the
-    # 512-key wave buckets fill their tables with ~512 distinct keys (2/3 of
-    # the 768 slots: the longest probe runs)
+    # wave buckets (512 keys; 256 two-word keys for k > 32) fill their tables
+    # with as many distinct keys (2/3 of the 768 / 384 slots: the longest
+    # probe runs)
     monkeypatch.setenv("FASTKMER_WAVE_SLOTS", slots)
     fasta = fk.synth_fasta(100_000, 100, 3_000_000_000, seed=61)
-    kc = run_counter(fasta, 28, 10, 3, 64)
-    ref = oracle.OracleResult(fasta, 28, 10, 64)
+    kc = run_counter(fasta, k, m, 3, 64)
+    ref = oracle.OracleResult(fasta, k, m, 64)
     assert kc.stats()["distinct"] > 0.95 * ref.total_kmers
     assert_same_as_oracle(kc, ref)
 
