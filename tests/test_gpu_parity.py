@@ -406,6 +406,20 @@ def test_full_size_properties():
     assert st["kmers"] > 0.9 * n_reads * 73
 
 
+@pytest.mark.parametrize("k,m", [(28, 10), (55, 12)])
+def test_max_fine_bits_one_bin_vs_oracle(k, m):
+    # B = 1: every k-mer in one bin (4.4 M at k = 28, 2.8 M at k = 55), past 2^14 cells of the
+    # cell target, so the bin is cut into the most cells (F = MAX_FINE_BITS = 15: the histogram,
+    # flag and scatter kernels at 128 KB of LDS) -- the largest-F path against the oracle
+    fasta = fk.synth_fasta(60_000, 100, 10_000_000, seed=67)
+    kc = run_counter(fasta, k, m, 3, 1)
+    st = kc.stats()
+    assert st["fine_bits"] == 15
+    ref = oracle.OracleResult(fasta, k, m, 1)
+    assert st["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref)
+
+
 def test_big_bins_two_level_vs_oracle():
     # few, large bins (~800K k-mers each): 2^11 cells per bin, 32 super-cells
     # (the two-level expansion with F1 > 0) and all three count tiers
