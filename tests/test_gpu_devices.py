@@ -66,3 +66,38 @@ def test_two_devices_interleaved_in_one_thread():
     ka.close()
     kb.close()
     torch.cuda.set_device(0)
+
+
+def test_device_input_then_host_input_on_one_context():
+    # a context that mapped a borrowed device buffer (fk_ingest_device) takes host input for its
+    # next job, and device input again after that (the JNI shim reuses one context per executor)
+    fasta = _fasta(24)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    buf = torch.frombuffer(bytearray(fasta), dtype=torch.uint8).to("cuda")
+    torch.cuda.synchronize()
+    with fk.KmerCounter(28, 10, 3, 2048, False, 0) as kc:
+        kc.ingest_device(buf.data_ptr(), buf.numel())
+        kc.finish()
+        assert_same_as_oracle(kc, ref)
+        kc.ingest(fasta)
+        kc.finish()
+        assert_same_as_oracle(kc, ref)
+        kc.ingest_device(buf.data_ptr(), buf.numel())
+        kc.finish()
+        assert_same_as_oracle(kc, ref)
+
+
+def test_bin_owners_rejected_with_grouped_emit():
+    # fk_set_bin_owners after fk_set_grouped_emit: the emitted layout would not match the counts
+    # handed to the all-to-all, so the call fails (FK_E_STATE) and the context stays usable
+    fasta = _fasta(25)
+    with fk.KmerCounter(28, 10, 3, 2048, False, 0, n_ranks=2, rank=0) as kc:
+        kc.ingest(fasta)
+        kc.set_grouped_emit(True)
+        kc.map()
+        with pytest.raises(fk.FastKmerError):
+            kc.set_bin_owners([b % 2 for b in range(2048)])
+        kc.set_grouped_emit(False)  # toggling the emit layout asks for a new fk_map
+        kc.map()
+        counts = kc.set_bin_owners([(b + 1) % 2 for b in range(2048)])
+        assert len(counts) == 2 and sum(counts) > 0
