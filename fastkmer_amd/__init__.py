@@ -53,7 +53,12 @@ class fk_stats(ctypes.Structure):
                 ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
                  "ms_signature_kernel")] + [("fused_map", ctypes.c_uint64), ("ms_h2d", ctypes.c_double),
                                        ("fused_fallback", ctypes.c_uint64),
-                                       ("ht_spilled", ctypes.c_uint64), ("ht_rounds", ctypes.c_uint64)]
+                                       ("ht_spilled", ctypes.c_uint64), ("ht_rounds", ctypes.c_uint64),
+                                       ("xch_steps", ctypes.c_uint64), ("xch_bytes_sent", ctypes.c_uint64),
+                                       ("xch_bytes_received", ctypes.c_uint64), ("ms_exchange", ctypes.c_double),
+                                       ("ms_exchange_tail", ctypes.c_double)]
+
+COMM_ID_BYTES = 128
 
 
 _lib = None
@@ -124,6 +129,11 @@ def lib():
         "fk_signature_counts": (ctypes.c_int, [P, P, U64]),
         "fk_write_bin_signatures": (ctypes.c_int, [P, P, U64, ctypes.c_char_p]),
         "fk_find_bin_signatures": (ctypes.c_int, [P, ctypes.c_char_p]),
+        "fk_comm_unique_id": (ctypes.c_int, [P]),
+        "fk_comm_init": (ctypes.c_int, [P, P]),
+        "fk_comm_init_local": (ctypes.c_int, [P, I32]),
+        "fk_comm_transport": (ctypes.c_char_p, [P]),
+        "fk_exchange_plan": (ctypes.c_int, [I32, I32, P, P, U64, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -349,8 +359,23 @@ class KmerCounter:
                                        sr.shape[0], sr.shape[1]))
 
     def finish(self) -> None:
+        """Single rank: map + count.  With a communicator (comm_init / comm_init_local):
+        the last piece, the exchange with the other ranks, and the count of this rank's
+        bins -- collective, every rank of the job calls it."""
         self._sizes = None
         _check(lib().fk_finish(self._h))
+
+    # -- multi-GPU inside the library (fk_comm_*)
+    def comm_init(self, unique_id: bytes) -> None:
+        """Join the job's RCCL communicator (unique_id from comm_unique_id() on one rank)."""
+        if len(unique_id) != COMM_ID_BYTES:
+            raise ValueError(f"an RCCL unique id has {COMM_ID_BYTES} bytes")
+        buf = ctypes.create_string_buffer(bytes(unique_id), COMM_ID_BYTES)
+        _check(lib().fk_comm_init(self._h, buf))
+
+    @property
+    def comm_transport(self) -> str:
+        return lib().fk_comm_transport(self._h).decode()
 
     # -- results
     def bin_sizes(self) -> np.ndarray:
@@ -412,6 +437,36 @@ class KmerCounter:
         st = fk_stats()
         _check(lib().fk_get_stats(self._h, ctypes.byref(st)))
         return {n: getattr(st, n) for n, _ in fk_stats._fields_}
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (fk_comm_unique_id): made on one rank, handed to all."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().fk_comm_unique_id(buf))
+    return buf.raw
+
+
+def comm_init_local(counters) -> None:
+    """Join KmerCounters of this process (ranks 0..n-1) into one in-process group
+    (fk_comm_init_local); drive each from its own thread."""
+    arr = (ctypes.c_void_p * len(counters))(*[c._h.value for c in counters])
+    _check(lib().fk_comm_init_local(arr, len(counters)))
+
+
+def exchange_plan(sent, received, record_bytes: int):
+    """fk_exchange_plan: one exchange step's send / receive byte blocks.
+    sent / received: [n_ranks, 2 * parts + 1] u64 messages.  Returns
+    (send_off, send_bytes, recv_off, recv_bytes, all_final)."""
+    snd = np.ascontiguousarray(sent, dtype=np.uint64)
+    rcv = np.ascontiguousarray(received, dtype=np.uint64)
+    if snd.ndim != 2 or snd.shape != rcv.shape or snd.shape[1] % 2 != 1:
+        raise ValueError("sent / received must be [n_ranks, 2 * parts + 1] arrays of one shape")
+    n, parts = snd.shape[0], (snd.shape[1] - 1) // 2
+    so, sb, ro, rb = (np.zeros(n, dtype=np.uint64) for _ in range(4))
+    fin = ctypes.c_int32(0)
+    _check(lib().fk_exchange_plan(n, parts, snd.ctypes.data, rcv.ctypes.data, record_bytes, so.ctypes.data,
+                                  sb.ctypes.data, ro.ctypes.data, rb.ctypes.data, ctypes.byref(fin)))
+    return so, sb, ro, rb, bool(fin.value)
 
 
 def lpt_owners(sizes, n_ranks: int) -> np.ndarray:

@@ -20,8 +20,8 @@ CLI = os.path.join(PKG, "bin", "fastkmer-cli")
 ARCH = os.environ.get("FASTKMER_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-LIB_SOURCES = ["fk_kernels.hip", "fk_api.cpp"]
-DEPS = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".inc", ".h")) or f == "fk_api.cpp")
+LIB_SOURCES = ["fk_kernels.hip", "fk_api.cpp", "fk_comm.cpp"]
+DEPS = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".inc", ".h")) or f in ("fk_api.cpp", "fk_comm.cpp"))
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -97,7 +97,7 @@ def build(force: bool = False) -> str:
                 _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
                       "-Wall", "-Wno-unused-function", "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj])
             objs.append(obj)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-ldl"])
         for o in objs:
             os.remove(o)
     if force or _stale(CLI, [os.path.join(CSRC, "fk_cli.cpp"), LIB]):

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/fastkmer.h"
+#include "fk_comm.h"
 #include "fk_internal.h"
 
 #define FK_EXPORT extern "C" __attribute__((visibility("default")))
@@ -236,6 +237,7 @@ struct fk_ctx {
     // input
     // host ingest: bytes are streamed to fasta_own (appended until the next fk_map)
     bool ingest_fresh = true;        // the next fk_ingest starts a new input
+    bool dev_open = false;           // fk_ingest_device(..., last = 0): the borrowed input is unfinished
     void *pinned[2] = {nullptr, nullptr};  // staging for pageable sources
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr;     // H2D of fk_ingest (the map runs on `stream` meanwhile)
@@ -286,6 +288,34 @@ struct fk_ctx {
     hipEvent_t ev[12] = {};
     double ms_h2d = 0.0;  // last fk_ingest: first copy issued -> last copy done
     bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
+    std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
+
+    // multi-rank exchange inside the context (fk_comm_init / fk_comm_init_local): the input
+    // is emitted in pieces grouped by (destination, local bin) and each piece is exchanged
+    // while the next one is still being copied in; fk_finish sends the last piece, then
+    // counts every received segment (the reduceByKey shuffle of SBKC:1034-1042)
+    fk::Comm *comm = nullptr;
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t emit_ev = nullptr;                // map stream: a piece's send records are written
+    std::vector<hipEvent_t> xev;                 // comm stream: begin / end of every piece's transfer
+    uint64_t piece_bytes = 1ull << 30;           // FASTKMER_PIECE_BYTES: FASTA bytes per piece
+    uint64_t ingest_seg = 32ull << 20;           // FASTKMER_INGEST_SEG: H2D segment of a pinned source
+    DevBuf xsend, xrecv;                         // send ring (pieces in flight), received records
+    struct XSeg {                                // received records of one (piece, sender)
+        uint64_t off;                            // first record in xrecv
+        int32_t sender;
+        std::vector<uint64_t> rec, kmer;         // per local bin
+    };
+    struct Xch {
+        bool open = false;           // a job's exchange has started (pieces sent)
+        bool sent_final = false;     // this rank has sent its last piece
+        bool all_final = false;      // every rank has sent its last piece
+        bool stop_pieces = false;    // the fused map fell back: the rest goes in fk_finish, earlier pieces retracted
+        uint64_t tiles_sent = 0;     // tiled records [0, tiles_sent) emitted in pieces
+        uint64_t send_used = 0, recv_used = 0;  // records
+        uint64_t pieces = 0, bytes_sent = 0, bytes_received = 0, expect_bytes = 0;
+        std::vector<XSeg> segs;
+    } xch;
 };
 
 // ---------------------------------------------------------------------------
@@ -429,6 +459,10 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (lh && lh[0]) c->lh_mode = atoi(lh);
     const char *lp = getenv("FASTKMER_LH_PROBE");
     if (lp && lp[0]) c->lh_probe = atoi(lp);
+    if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0])
+        c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
+    if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
+        c->ingest_seg = std::max(1ull << 16, strtoull(sg, nullptr, 10));
     const char *cm = getenv("FASTKMER_COUNT_MODE");
     if (cm && cm[0]) c->count_mode = atoi(cm);
     if (cfg->device >= 0) {
@@ -493,6 +527,17 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
         if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
     }
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    delete c->comm;
+    c->comm = nullptr;
+    release(c->xsend);
+    release(c->xrecv);
+    for (auto &e : c->xev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : c->seg_evs)
+        if (e) (void)hipEventDestroy(e);
+    if (c->emit_ev) (void)hipEventDestroy(c->emit_ev);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     c->dest.release_all();
     c->part.release_all();
     c->binhist.release_all();
@@ -541,7 +586,6 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 constexpr size_t PIN_CHUNK = 32ull << 20;  // pinned staging buffer (x2) for pageable sources
-constexpr size_t INGEST_SEG = 32ull << 20;  // H2D segment: the tiles it completes are mapped while the next lands
 
 // Grows b to at least `bytes`, keeping its first `keep` bytes (stream-ordered copy).
 static int grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s) {
@@ -582,6 +626,9 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     return FK_OK;
 }
 
+static int xch_maybe_piece(fk_ctx *c);
+static void xch_reset(fk_ctx *c);
+
 // Appends host bytes to the device input on the copy stream, in segments.
 // Pinned sources are copied by DMA directly; pageable ones through two
 // pinned staging buffers (the memcpy of one overlapping the DMA of the
@@ -596,7 +643,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>()) {
         // a borrowed device input (fk_ingest_device): host chunks cannot be appended
         // to it, but a host ingest that starts a new job replaces it
-        if (!c->ingest_fresh) return set_err(FK_E_STATE, "fk_ingest appending to an fk_ingest_device input");
+        if (c->dev_open) return set_err(FK_E_STATE, "fk_ingest appending to an fk_ingest_device input");
         c->d_fasta = nullptr;
     }
     hipStream_t s = c->stream, cs = c->copy_stream;
@@ -604,6 +651,11 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     if (fresh) {
         c->n_fasta = 0;
         c->ingest_fresh = false;
+        if (c->comm) {
+            if (c->xch.open) return set_err(FK_E_STATE, "fk_ingest: the previous job's exchange is unfinished (fk_finish)");
+            HIP_TRY(hipStreamSynchronize(c->comm_stream));
+            xch_reset(c);
+        }
         HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
         c->pm_active = premap_eligible(c);
         c->pm_tiles = 0;
@@ -642,26 +694,52 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
                 HIP_TRY(hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
                 HIP_TRY(hipEventRecord(c->pin_ev[i], cs));
             }
+    // with a communicator, every piece of mapped tiles is exchanged while later ones land
+    const bool pieces = c->comm && c->pm_active;
+    if (pieces && fresh) c->xch.expect_bytes = last ? n : 0;
     HIP_TRY(hipEventRecord(c->h2d_ev[0], cs));
-    size_t off = 0;
-    for (int i = 0; off < n; ++i) {
-        const size_t len = std::min(pinned ? INGEST_SEG : PIN_CHUNK, n - off);
-        if (pinned) {
+    if (pinned) {
+        // every segment's copy is queued first, so the DMA runs back to back even while the
+        // host waits on a piece's exchange
+        const size_t seg = c->ingest_seg, nseg = (n + seg - 1) / seg;
+        while (c->pm_active && c->seg_evs.size() < nseg) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->seg_evs.push_back(e);
+        }
+        size_t off = 0;
+        for (size_t i = 0; off < n; ++i) {
+            const size_t len = std::min(seg, n - off);
             HIP_TRY(hipMemcpyAsync(dst + off, fasta + off, len, hipMemcpyHostToDevice, cs));
-        } else {
+            if (c->pm_active) HIP_TRY(hipEventRecord(c->seg_evs[i], cs));
+            off += len;
+        }
+        HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
+        off = 0;
+        for (size_t i = 0; c->pm_active && off < n; ++i) {
+            off += std::min(seg, n - off);
+            HIP_TRY(hipStreamWaitEvent(s, c->seg_evs[i], 0));
+            FK_TRY(premap_launch(c, have + off, last && off == n));
+            if (pieces) FK_TRY(xch_maybe_piece(c));
+        }
+    } else {
+        size_t off = 0;
+        for (int i = 0; off < n; ++i) {
+            const size_t len = std::min(PIN_CHUNK, n - off);
             HIP_TRY(hipEventSynchronize(c->pin_ev[i & 1]));  // its previous DMA is done
             memcpy(c->pinned[i & 1], fasta + off, len);
             HIP_TRY(hipMemcpyAsync(dst + off, c->pinned[i & 1], len, hipMemcpyHostToDevice, cs));
             HIP_TRY(hipEventRecord(c->pin_ev[i & 1], cs));
+            off += len;
+            if (c->pm_active) {
+                HIP_TRY(hipEventRecord(c->seg_ev, cs));
+                HIP_TRY(hipStreamWaitEvent(s, c->seg_ev, 0));
+                FK_TRY(premap_launch(c, have + off, last && off == n));
+                if (pieces) FK_TRY(xch_maybe_piece(c));
+            }
         }
-        off += len;
-        if (c->pm_active) {
-            HIP_TRY(hipEventRecord(c->seg_ev, cs));
-            HIP_TRY(hipStreamWaitEvent(s, c->seg_ev, 0));
-            FK_TRY(premap_launch(c, have + off, last && off == n));
-        }
+        HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
     }
-    HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
     if (c->pm_active && last) {
         c->pm_last_seen = true;
         if (n == 0) FK_TRY(premap_launch(c, need, true));
@@ -689,9 +767,11 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
 }
 
 FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
-    (void)last;
     if (!c || (!d && n)) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
+    if (c->comm && c->xch.open) return set_err(FK_E_STATE, "fk_ingest_device: the previous job's exchange is unfinished");
+    if (c->comm) xch_reset(c);
+    c->dev_open = last == 0;  // a borrowed input takes no appended host chunks
     c->ingest_fresh = true;
     c->pm_active = false;
     reset_results(c);
@@ -723,8 +803,11 @@ FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_r
     const SynthParams p = make_synth(first_read, n_reads, read_len, genome_len, seed, err_rate, n_rate);
     const uint64_t nb = n_reads * p.rec_bytes;
     FK_TRY(ensure(c->fasta_own, nb));
+    if (c->comm && c->xch.open) return set_err(FK_E_STATE, "fk_synth_fasta_device: the previous job's exchange is unfinished");
+    if (c->comm) xch_reset(c);
     HIP_TRY(launch_synth(c->fasta_own.as<uint8_t>(), nb, p, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->dev_open = false;
     c->ingest_fresh = true;
     c->pm_active = false;
     c->d_fasta = c->fasta_own.as<uint8_t>();
@@ -793,12 +876,12 @@ static RecSrc map_src(const fk_ctx *c) {
     return dense_src(c->records.as<uint64_t>(), c->nrec, c->W);
 }
 
-FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
-    if (!c) return set_err(FK_E_INVALID, "null ctx");
-    DeviceGuard dg_(c->device);
+// fk_map steps 0-2: the input's super-k-mer records (fused kernel, or parse + signature)
+static int map_records(fk_ctx *c) {
     const double t_start = now_ms();
     hipStream_t s = c->stream;
     c->ingest_fresh = true;  // a later fk_ingest starts a new input
+    c->dev_open = false;
     const uint64_t n = c->d_fasta ? c->n_fasta : 0;
     reset_results(c);
     c->stats = fk_stats{};
@@ -923,6 +1006,16 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     }
     c->stats.kmers = c->nkmers;
     c->stats.superkmers = c->nrec;
+    c->stats.ms_total += now_ms() - t_start;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    DeviceGuard dg_(c->device);
+    FK_TRY(map_records(c));
+    const double t_start = now_ms();
+    hipStream_t s = c->stream;
 
     // 3a. destination histogram (records per rank)
     c->send_counts.assign(c->G, 0);
@@ -1593,6 +1686,19 @@ FK_EXPORT int fk_map_part_counts(fk_ctx *c, uint64_t *records, uint64_t *kmers) 
     return FK_OK;
 }
 
+// Counts records that arrive grouped by local bin: ranges[lb] = the bin's record ranges in d_recv.
+static int reduce_ranges(fk_ctx *c, const uint64_t *d_recv, uint64_t nrecv,
+                         const std::vector<std::vector<std::pair<uint64_t, uint64_t>>> &ranges,
+                         const std::vector<uint64_t> &bkm, double t0) {
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    build_chunks(c->nlb, ranges, chunks, bcb);
+    FK_TRY(upload_chunks(c, chunks, bcb));
+    HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+    c->rsrc = d_recv;
+    return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
+}
+
 FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, const uint64_t *seg_records,
                                 const uint64_t *seg_kmers, int32_t nseg, int32_t parts_per_seg) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
@@ -1625,22 +1731,330 @@ FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, c
     if (off != nrecv)
         return set_err(FK_E_INVALID, "segment table holds %llu records, buffer %llu", (unsigned long long)off,
                        (unsigned long long)nrecv);
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> bcb;
-    build_chunks(nlb, ranges, chunks, bcb);
-    FK_TRY(upload_chunks(c, chunks, bcb));
-    HIP_TRY(hipEventRecord(c->ev[5], s));
-    c->rsrc = (const uint64_t *)d_recv;
-    return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
+    return reduce_ranges(c, (const uint64_t *)d_recv, nrecv, ranges, bkm, t0);
+}
+
+// ---------------------------------------------------------------------------
+// multi-rank exchange inside the context (fk_comm_init*)
+// ---------------------------------------------------------------------------
+
+enum : uint64_t { XF_FINAL = 1, XF_RETRACT = 2 };
+
+// Host arithmetic of one exchange step (fk_exchange_plan): byte offsets and sizes of the send
+// blocks (destination-major, as the grouped emit writes them) and of the receive blocks
+// (sender-major), and whether every sender has sent its last piece.
+static int plan_step(uint32_t G, uint32_t L, const uint64_t *sent, const uint64_t *got, uint64_t rb, uint64_t *soff,
+                     uint64_t *sbytes, uint64_t *roff, uint64_t *rbytes, bool *all_final) {
+    const size_t msg = 2 * (size_t)L + 1;
+    uint64_t so = 0, ro = 0;
+    bool fin = true;
+    for (uint32_t d = 0; d < G; ++d) {
+        uint64_t ns = 0, nr = 0;
+        for (uint32_t lb = 0; lb < L; ++lb) {
+            ns += sent[d * msg + lb];
+            nr += got[d * msg + lb];
+        }
+        const uint64_t fs = sent[d * msg + 2 * L], fr = got[d * msg + 2 * L];
+        if ((fs | fr) & ~(XF_FINAL | XF_RETRACT)) return set_err(FK_E_INVALID, "exchange step: unknown flag bits");
+        if ((fr & XF_RETRACT) && !(fr & XF_FINAL))
+            return set_err(FK_E_INVALID, "exchange step: rank %u retracts outside its last piece", d);
+        fin = fin && (fr & XF_FINAL);
+        soff[d] = so;
+        sbytes[d] = ns * rb;
+        roff[d] = ro;
+        rbytes[d] = nr * rb;
+        so += ns * rb;
+        ro += nr * rb;
+    }
+    *all_final = fin;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_exchange_plan(int32_t n_ranks, int32_t parts, const uint64_t *sent, const uint64_t *received,
+                               uint64_t record_bytes, uint64_t *send_off, uint64_t *send_bytes, uint64_t *recv_off,
+                               uint64_t *recv_bytes, int32_t *all_final) {
+    if (n_ranks < 1 || parts < 0 || !sent || !received || !send_off || !send_bytes || !recv_off || !recv_bytes ||
+        !all_final)
+        return set_err(FK_E_INVALID, "bad argument");
+    bool fin = false;
+    FK_TRY(plan_step((uint32_t)n_ranks, (uint32_t)parts, sent, received, record_bytes, send_off, send_bytes, recv_off,
+                     recv_bytes, &fin));
+    *all_final = fin ? 1 : 0;
+    return FK_OK;
+}
+
+static void xch_reset(fk_ctx *c) {
+    c->xch = fk_ctx::Xch{};
+}
+
+static int comm_fail(fk_ctx *c, int rc) {
+    if (c->comm) c->comm->abort();  // peers blocked in a step return instead of waiting
+    return rc;
+}
+
+static hipEvent_t xch_event(fk_ctx *c, size_t i) {
+    while (c->xev.size() <= i) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        c->xev.push_back(e);
+    }
+    return c->xev[i];
+}
+
+// One exchange step; collective (every rank runs its steps in the same sequence, whatever each
+// step carries).  src = this rank's records of the step (null: none): grouped by (destination,
+// local bin) into the send ring, their per-part counts and `flags` all-to-all'ed, then the
+// records posted on the comm stream (they move while the map stream goes on); the received
+// blocks become segments of the count.  `expect` = records expected in all (sizes xrecv).
+static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
+    hipStream_t s = c->stream, cs = c->comm_stream;
+    const uint32_t G = c->G, L = c->grp_nlb, nparts = G * L;
+    const uint64_t rb = (uint64_t)c->W * 8;
+    const size_t msg = 2 * (size_t)L + 1;
+    std::vector<uint64_t> pr(nparts, 0), pk(nparts, 0);
+    uint64_t piece_rec = 0;
+    if (src && src->nrec && src->ntiles) {
+        FK_TRY(part_count(c->dest, *src, 0, G, c->grp_table.as<uint32_t>(), nparts, c->ws, s));
+        HIP_TRY(hipMemcpyAsync(pr.data(), c->dest.rec.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(pk.data(), c->dest.kmer.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (uint64_t v : pr) piece_rec += v;
+    }
+    if (piece_rec) {
+        // send ring: earlier pieces are read by the comm stream; wrap around once it has drained
+        if ((c->xch.send_used + piece_rec) * rb > c->xsend.bytes) {
+            HIP_TRY(hipStreamSynchronize(cs));
+            c->xch.send_used = 0;
+            FK_TRY(ensure(c->xsend, piece_rec * rb * 2));
+        }
+        FK_TRY(part_scatter(c->dest, 0, G, c->grp_table.as<uint32_t>(), c->xsend.as<uint64_t>() + c->xch.send_used * c->W,
+                            s));
+        HIP_TRY(hipEventRecord(c->emit_ev, s));
+    }
+    std::vector<uint64_t> out((size_t)G * msg), in((size_t)G * msg);
+    for (uint32_t d = 0; d < G; ++d) {
+        for (uint32_t lb = 0; lb < L; ++lb) {
+            out[d * msg + lb] = pr[(size_t)d * L + lb];
+            out[d * msg + L + lb] = pk[(size_t)d * L + lb];
+        }
+        out[d * msg + 2 * L] = flags;
+    }
+    std::string err;
+    if (c->comm->alltoall_u64(out.data(), in.data(), msg, cs, err))
+        return set_err(FK_E_DEVICE, "exchange step %llu, counts: %s", (unsigned long long)c->xch.pieces, err.c_str());
+    std::vector<uint64_t> soff(G), sbytes(G), roff(G), rbytes(G);
+    bool all_final = false;
+    FK_TRY(plan_step(G, L, out.data(), in.data(), rb, soff.data(), sbytes.data(), roff.data(), rbytes.data(), &all_final));
+    uint64_t recv_rec = 0;
+    for (uint32_t r = 0; r < G; ++r) recv_rec += rbytes[r] / rb;
+    if ((c->xch.recv_used + recv_rec) * rb > c->xrecv.bytes) {
+        // the received records stay until the count: grow, keeping them (sized for the whole input
+        // once the first pieces show the records per FASTA byte)
+        uint64_t want = c->xch.recv_used + recv_rec;
+        if (c->xch.expect_bytes && c->xch.tiles_sent) {
+            const double covered = (double)c->xch.tiles_sent * (double)fm_tile_bytes(c->fused_nt);
+            want = std::max<uint64_t>(want, (uint64_t)((double)want * (double)c->xch.expect_bytes / covered * 1.1));
+        }
+        HIP_TRY(hipStreamSynchronize(cs));
+        FK_TRY(grow_keep(c->xrecv, want * rb, c->xch.recv_used * rb, s));
+    }
+    const size_t step = (size_t)c->xch.pieces;
+    hipEvent_t e0 = xch_event(c, 2 * step), e1 = xch_event(c, 2 * step + 1);
+    if (!e0 || !e1) return set_err(FK_E_DEVICE, "hipEventCreate failed");
+    if (piece_rec) HIP_TRY(hipStreamWaitEvent(cs, c->emit_ev, 0));
+    HIP_TRY(hipEventRecord(e0, cs));
+    if (c->comm->alltoallv(c->xsend.as<uint8_t>() + c->xch.send_used * rb, soff.data(), sbytes.data(),
+                           c->xrecv.as<uint8_t>() + c->xch.recv_used * rb, roff.data(), rbytes.data(), cs, err))
+        return set_err(FK_E_DEVICE, "exchange step %llu, records: %s", (unsigned long long)step, err.c_str());
+    HIP_TRY(hipEventRecord(e1, cs));
+    for (uint32_t r = 0; r < G; ++r) {
+        const uint64_t *m = in.data() + (size_t)r * msg;
+        if (m[2 * L] & XF_RETRACT) {  // the sender mapped again from scratch: its earlier pieces are void
+            auto &v = c->xch.segs;
+            v.erase(std::remove_if(v.begin(), v.end(), [&](const fk_ctx::XSeg &g) { return g.sender == (int32_t)r; }),
+                    v.end());
+        }
+        if (!rbytes[r]) continue;
+        fk_ctx::XSeg g;
+        g.off = c->xch.recv_used + roff[r] / rb;
+        g.sender = (int32_t)r;
+        g.rec.assign(m, m + L);
+        g.kmer.assign(m + L, m + 2 * L);
+        c->xch.segs.push_back(std::move(g));
+        if (r != (uint32_t)c->cfg.rank) c->xch.bytes_received += rbytes[r];
+    }
+    for (uint32_t d = 0; d < G; ++d)
+        if (d != (uint32_t)c->cfg.rank) c->xch.bytes_sent += sbytes[d];
+    c->xch.send_used += piece_rec;
+    c->xch.recv_used += recv_rec;
+    c->xch.pieces += 1;
+    c->xch.open = true;
+    c->xch.all_final = all_final;
+    if (flags & XF_FINAL) c->xch.sent_final = true;
+    return FK_OK;
+}
+
+// fk_ingest: sends the tiles mapped since the last piece once they cover a piece.  The fused
+// map's fallback flag is read first: a flagged input is mapped again in fk_finish and sent
+// whole, retracting the pieces sent so far.
+static int xch_maybe_piece(fk_ctx *c) {
+    if (c->xch.stop_pieces || c->xch.sent_final) return FK_OK;
+    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    if ((c->pm_tiles - c->xch.tiles_sent) * tile < c->piece_bytes) return FK_OK;
+    uint64_t h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[2]) {
+        c->xch.stop_pieces = true;
+        return FK_OK;
+    }
+    const uint64_t t0 = c->xch.tiles_sent, nt = c->pm_tiles - t0;
+    const uint32_t tcap = map_fused_tcap();
+    const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
+                                 nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
+    c->xch.tiles_sent = c->pm_tiles;
+    const int rc = xch_step(c, &src, 0);
+    return rc ? comm_fail(c, rc) : FK_OK;
+}
+
+// fk_finish with a communicator: the last piece, the closing steps, then the count of every
+// received segment.
+static int finish_exchange(fk_ctx *c) {
+    const double t0 = now_ms();
+    hipStream_t s = c->stream, cs = c->comm_stream;
+    const bool pieced = c->xch.tiles_sent > 0;
+    const uint64_t tiles_sent = c->xch.tiles_sent;
+    FK_TRY(map_records(c));
+    RecSrc src;
+    uint64_t flags = XF_FINAL;
+    if (c->rec_tiled && pieced && !c->xch.stop_pieces && tiles_sent <= c->rec_tiles) {
+        const uint64_t nt = c->rec_tiles - tiles_sent;
+        const uint32_t tcap = map_fused_tcap();
+        src = tiled_src(c->records.as<uint64_t>() + tiles_sent * tcap * c->W, c->tcnt.as<uint32_t>() + tiles_sent,
+                        nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + tiles_sent * tcap);
+    } else {
+        src = map_src(c);
+        if (pieced) flags |= XF_RETRACT;
+    }
+    c->mapped = true;
+    int rc = xch_step(c, &src, flags);
+    const size_t last_step = (size_t)c->xch.pieces - 1;
+    while (!rc && !c->xch.all_final) rc = xch_step(c, nullptr, XF_FINAL);
+    if (rc) return comm_fail(c, rc);
+    HIP_TRY(hipEventRecord(c->ev[4], cs));  // every rank's records have landed
+    HIP_TRY(hipStreamWaitEvent(s, c->ev[4], 0));
+    // segments, bin after bin inside each: the ranges of every local bin
+    const uint32_t nlb = c->nlb;
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
+    std::vector<uint64_t> bkm(nlb, 0);
+    uint64_t nrecv = 0;
+    for (const auto &g : c->xch.segs) {
+        uint64_t off = g.off;
+        for (uint32_t lb = 0; lb < c->grp_nlb; ++lb) {
+            const uint64_t n = g.rec[lb];
+            if (n && lb >= nlb) return set_err(FK_E_INVALID, "records for local bin %u of %u", lb, nlb);
+            if (n) {
+                ranges[lb].push_back({off, off + n});
+                bkm[lb] += g.kmer[lb];
+                nrecv += n;
+            }
+            off += n;
+        }
+    }
+    FK_TRY(reduce_ranges(c, c->xrecv.as<uint64_t>(), nrecv, ranges, bkm, t0));
+    // exchange figures (every transfer has completed: the count waited for them)
+    double ms = 0.0;
+    for (size_t i = 0; i < (size_t)c->xch.pieces; ++i) ms += ev_ms(c->xev[2 * i], c->xev[2 * i + 1]);
+    c->stats.xch_steps = c->xch.pieces;
+    c->stats.xch_bytes_sent = c->xch.bytes_sent;
+    c->stats.xch_bytes_received = c->xch.bytes_received;
+    c->stats.ms_exchange = ms;
+    c->stats.ms_exchange_tail = ev_ms(c->xev[2 * last_step], c->xev[2 * ((size_t)c->xch.pieces - 1) + 1]);
+    c->stats.records_received = nrecv;
+    xch_reset(c);
+    return FK_OK;
 }
 
 FK_EXPORT int fk_finish(fk_ctx *c) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
-    if (c->G != 1) return set_err(FK_E_STATE, "fk_finish is the single-rank path; use fk_map/fk_map_emit/fk_reduce");
+    if (c->comm) {
+        DeviceGuard dg_(c->device);
+        return finish_exchange(c);
+    }
+    if (c->G != 1)
+        return set_err(FK_E_STATE, "fk_finish over %u ranks needs a communicator (fk_comm_init); or use "
+                                   "fk_map/fk_map_emit/fk_reduce", c->G);
     FK_TRY(fk_map(c, nullptr));
     DeviceGuard dg_(c->device);
     return reduce_src(c, map_src(c));
 }
+
+static int attach_comm(fk_ctx *c, fk::Comm *comm) {
+    DeviceGuard dg_(c->device);
+    if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (!c->emit_ev) HIP_TRY(hipEventCreateWithFlags(&c->emit_ev, hipEventDisableTiming));
+    c->comm = comm;
+    FK_TRY(fk_set_grouped_emit(c, 1));  // records leave grouped by (owner rank, local bin)
+    xch_reset(c);
+    return FK_OK;
+}
+
+FK_EXPORT int fk_comm_unique_id(uint8_t *id) {
+    if (!id) return set_err(FK_E_INVALID, "null argument");
+    std::string err;
+    if (fk::comm_unique_id(id, err)) return set_err(FK_E_DEVICE, "%s", err.c_str());
+    return FK_OK;
+}
+
+FK_EXPORT int fk_comm_init(fk_ctx *c, const uint8_t *id) {
+    if (!c || !id) return set_err(FK_E_INVALID, "null argument");
+    if (c->comm) return set_err(FK_E_STATE, "the context already has a communicator");
+    if (c->custom_owners) return set_err(FK_E_STATE, "the exchange uses the default placement (bin %% n_ranks)");
+    DeviceGuard dg_(c->device);
+    std::string err;
+    fk::Comm *comm = fk::comm_create_rccl(id, (int)c->G, c->cfg.rank, c->device, err);
+    if (!comm) return set_err(FK_E_DEVICE, "%s", err.c_str());
+    const int rc = attach_comm(c, comm);
+    if (rc) {
+        delete comm;
+        c->comm = nullptr;
+    }
+    return rc;
+}
+
+FK_EXPORT int fk_comm_init_local(fk_ctx **ctxs, int32_t n) {
+    if (!ctxs || n < 1) return set_err(FK_E_INVALID, "bad argument");
+    std::vector<int> devs(n);
+    for (int32_t r = 0; r < n; ++r) {
+        fk_ctx *c = ctxs[r];
+        if (!c) return set_err(FK_E_INVALID, "null context %d", r);
+        if (c->G != (uint32_t)n || c->cfg.rank != r)
+            return set_err(FK_E_INVALID, "context %d has rank %d of %u; expected rank %d of %d", r, c->cfg.rank, c->G,
+                           r, n);
+        if (c->comm) return set_err(FK_E_STATE, "context %d already has a communicator", r);
+        if (c->custom_owners) return set_err(FK_E_STATE, "the exchange uses the default placement (bin %% n_ranks)");
+        devs[r] = c->device;
+    }
+    std::vector<fk::Comm *> comms(n, nullptr);
+    std::string err;
+    if (fk::comm_create_local(n, devs.data(), comms.data(), err)) return set_err(FK_E_DEVICE, "%s", err.c_str());
+    for (int32_t r = 0; r < n; ++r) {
+        const int rc = attach_comm(ctxs[r], comms[r]);
+        if (rc) {
+            for (int32_t q = 0; q < n; ++q) {
+                if (ctxs[q]->comm == comms[q]) ctxs[q]->comm = nullptr;
+                delete comms[q];
+            }
+            return rc;
+        }
+    }
+    return FK_OK;
+}
+
+FK_EXPORT const char *fk_comm_transport(const fk_ctx *c) { return c && c->comm ? c->comm->kind() : ""; }
 
 // ---------------------------------------------------------------------------
 // results

@@ -1,0 +1,404 @@
+// fk_comm.cpp -- transports of the bin exchange (see fk_comm.h).
+#include "fk_comm.h"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace fk {
+
+namespace {
+
+std::string hip_msg(const char *what, hipError_t e) {
+    (void)hipGetLastError();
+    return std::string(what) + ": " + hipGetErrorString(e);
+}
+
+#define COMM_HIP(expr)                                \
+    do {                                              \
+        hipError_t e_ = (expr);                       \
+        if (e_ != hipSuccess) {                       \
+            err = hip_msg(#expr, e_);                 \
+            return -1;                                \
+        }                                             \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// RCCL, resolved at run time
+// ---------------------------------------------------------------------------
+
+struct RcclApi {
+    void *handle = nullptr;
+    std::string path;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+std::mutex g_rccl_mu;
+RcclApi g_rccl;
+bool g_rccl_tried = false;
+std::string g_rccl_err;
+
+// The RCCL already mapped into the process first (torch's, bound to the same
+// HIP runtime as this library), then the system one.
+const RcclApi *rccl(std::string &err) {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (!g_rccl_tried) {
+        g_rccl_tried = true;
+        std::vector<std::pair<const char *, int>> tries;
+        const char *env = getenv("FASTKMER_RCCL_LIB");
+        if (env && env[0]) tries.push_back({env, RTLD_NOW | RTLD_LOCAL});
+        tries.push_back({"librccl.so.1", RTLD_NOW | RTLD_NOLOAD});
+        tries.push_back({"librccl.so", RTLD_NOW | RTLD_NOLOAD});
+        tries.push_back({"librccl.so.1", RTLD_NOW | RTLD_LOCAL});
+        tries.push_back({"/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL});
+        for (auto &t : tries) {
+            void *h = dlopen(t.first, t.second);
+            if (!h) continue;
+            RcclApi a;
+            a.handle = h;
+            a.path = t.first;
+#define SYM(field, name) a.field = reinterpret_cast<decltype(a.field)>(dlsym(h, name))
+            SYM(GetUniqueId, "ncclGetUniqueId");
+            SYM(CommInitRank, "ncclCommInitRank");
+            SYM(CommDestroy, "ncclCommDestroy");
+            SYM(CommAbort, "ncclCommAbort");
+            SYM(GroupStart, "ncclGroupStart");
+            SYM(GroupEnd, "ncclGroupEnd");
+            SYM(Send, "ncclSend");
+            SYM(Recv, "ncclRecv");
+            SYM(AllReduce, "ncclAllReduce");
+            SYM(GetErrorString, "ncclGetErrorString");
+#undef SYM
+            if (a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
+                a.AllReduce && a.GetErrorString) {
+                Dl_info info;
+                if (dladdr(reinterpret_cast<void *>(a.GetUniqueId), &info) && info.dli_fname) a.path = info.dli_fname;
+                g_rccl = a;
+                break;
+            }
+            g_rccl_err = std::string(t.first) + " lacks the RCCL entry points";
+        }
+        if (!g_rccl.handle && g_rccl_err.empty()) g_rccl_err = "librccl.so.1 could not be loaded";
+    }
+    if (!g_rccl.handle) {
+        err = g_rccl_err;
+        return nullptr;
+    }
+    return &g_rccl;
+}
+
+class RcclComm : public Comm {
+   public:
+    RcclComm(const RcclApi *api, ncclComm_t comm, int n, int rank) : api_(api), comm_(comm) {
+        n_ = n;
+        rank_ = rank;
+    }
+    ~RcclComm() override {
+        if (stage_) (void)hipFree(stage_);
+        if (comm_) (void)api_->CommDestroy(comm_);
+    }
+    const char *kind() const override { return "rccl"; }
+
+    int alltoall_u64(const uint64_t *in, uint64_t *out, size_t n, hipStream_t s, std::string &err) override {
+        const size_t bytes = (size_t)n_ * n * 8;
+        if (stage(2 * bytes, err)) return -1;
+        uint64_t *din = static_cast<uint64_t *>(stage_), *dout = din + (size_t)n_ * n;
+        COMM_HIP(hipMemcpyAsync(din, in, bytes, hipMemcpyHostToDevice, s));
+        if (nccl(api_->GroupStart(), err)) return -1;
+        for (int p = 0; p < n_; ++p) {
+            if (nccl(api_->Send(din + (size_t)p * n, n, ncclUint64, p, comm_, s), err)) return end_group(err);
+            if (nccl(api_->Recv(dout + (size_t)p * n, n, ncclUint64, p, comm_, s), err)) return end_group(err);
+        }
+        if (nccl(api_->GroupEnd(), err)) return -1;
+        COMM_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s));
+        COMM_HIP(hipStreamSynchronize(s));
+        return 0;
+    }
+
+    int allreduce_sum_u64(uint64_t *v, size_t n, hipStream_t s, std::string &err) override {
+        if (!n) return 0;
+        if (stage(n * 8, err)) return -1;
+        COMM_HIP(hipMemcpyAsync(stage_, v, n * 8, hipMemcpyHostToDevice, s));
+        if (nccl(api_->AllReduce(stage_, stage_, n, ncclUint64, ncclSum, comm_, s), err)) return -1;
+        COMM_HIP(hipMemcpyAsync(v, stage_, n * 8, hipMemcpyDeviceToHost, s));
+        COMM_HIP(hipStreamSynchronize(s));
+        return 0;
+    }
+
+    int alltoallv(const uint8_t *send, const uint64_t *soff, const uint64_t *sbytes, uint8_t *recv,
+                  const uint64_t *roff, const uint64_t *rbytes, hipStream_t s, std::string &err) override {
+        if (nccl(api_->GroupStart(), err)) return -1;
+        for (int p = 0; p < n_; ++p) {
+            // a pair with nothing to move posts nothing on either side (both know the size)
+            if (sbytes[p] && nccl(api_->Send(send + soff[p], sbytes[p], ncclUint8, p, comm_, s), err))
+                return end_group(err);
+            if (rbytes[p] && nccl(api_->Recv(recv + roff[p], rbytes[p], ncclUint8, p, comm_, s), err))
+                return end_group(err);
+        }
+        return nccl(api_->GroupEnd(), err);
+    }
+
+    void abort() override {
+        if (comm_ && api_->CommAbort) {
+            (void)api_->CommAbort(comm_);
+            comm_ = nullptr;
+        }
+    }
+
+   private:
+    int nccl(ncclResult_t r, std::string &err) {
+        if (r == ncclSuccess) return 0;
+        err = std::string("RCCL: ") + api_->GetErrorString(r);
+        return -1;
+    }
+    int end_group(std::string &err) {
+        std::string ignore;
+        (void)nccl(api_->GroupEnd(), ignore);
+        (void)err;
+        return -1;
+    }
+    int stage(size_t bytes, std::string &err) {
+        if (stage_bytes_ >= bytes) return 0;
+        if (stage_) (void)hipFree(stage_);
+        stage_ = nullptr;
+        stage_bytes_ = 0;
+        COMM_HIP(hipMalloc(&stage_, bytes));
+        stage_bytes_ = bytes;
+        return 0;
+    }
+    const RcclApi *api_;
+    ncclComm_t comm_;
+    void *stage_ = nullptr;
+    size_t stage_bytes_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// in-process group
+// ---------------------------------------------------------------------------
+
+struct LocalGroup {
+    explicit LocalGroup(int n) : n(n) {
+        for (auto &v : slot) v.resize(n);
+    }
+    struct Slot {
+        const uint64_t *in = nullptr;
+        const uint8_t *send = nullptr;
+        const uint64_t *soff = nullptr, *sbytes = nullptr;
+        hipEvent_t ready = nullptr, done = nullptr;
+        int device = 0;
+    };
+    int n;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;
+    int arrived = 0;
+    bool failed = false;
+    std::vector<Slot> slot[2];  // by collective parity: a slot is rewritten two collectives later
+
+    int barrier(std::string &err) {
+        std::unique_lock<std::mutex> lk(mu);
+        if (failed) {
+            err = "a rank of the in-process group failed";
+            return -1;
+        }
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g || failed; });
+        }
+        if (failed) {
+            err = "a rank of the in-process group failed";
+            return -1;
+        }
+        return 0;
+    }
+    void fail() {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = true;
+        cv.notify_all();
+    }
+};
+
+class LocalComm : public Comm {
+   public:
+    LocalComm(std::shared_ptr<LocalGroup> g, int rank, int device) : g_(std::move(g)), dev_(device) {
+        n_ = g_->n;
+        rank_ = rank;
+    }
+    ~LocalComm() override {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev_);
+        for (auto &e : ready_)
+            if (e) (void)hipEventDestroy(e);
+        for (auto &e : done_)
+            if (e) (void)hipEventDestroy(e);
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    int init(std::string &err) {
+        for (int i = 0; i < 2; ++i) {
+            COMM_HIP(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming));
+            COMM_HIP(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming));
+        }
+        return 0;
+    }
+    const char *kind() const override { return "local"; }
+
+    int alltoall_u64(const uint64_t *in, uint64_t *out, size_t n, hipStream_t, std::string &err) override {
+        auto &sl = g_->slot[next()];
+        sl[rank_].in = in;
+        if (g_->barrier(err)) return -1;
+        for (int s = 0; s < n_; ++s) memcpy(out + (size_t)s * n, sl[s].in + (size_t)rank_ * n, n * 8);
+        return g_->barrier(err);  // the peers' `in` arrays stay valid until everyone has read them
+    }
+
+    int allreduce_sum_u64(uint64_t *v, size_t n, hipStream_t, std::string &err) override {
+        std::vector<uint64_t> mine(v, v + n);
+        auto &sl = g_->slot[next()];
+        sl[rank_].in = mine.data();
+        if (g_->barrier(err)) return -1;
+        for (size_t i = 0; i < n; ++i) {
+            uint64_t t = 0;
+            for (int s = 0; s < n_; ++s) t += sl[s].in[i];
+            v[i] = t;
+        }
+        return g_->barrier(err);
+    }
+
+    int alltoallv(const uint8_t *send, const uint64_t *soff, const uint64_t *sbytes, uint8_t *recv,
+                  const uint64_t *roff, const uint64_t *rbytes, hipStream_t s, std::string &err) override {
+        const int p = next();
+        auto &sl = g_->slot[p];
+        COMM_HIP(hipEventRecord(ready_[p], s));
+        sl[rank_].send = send;
+        sl[rank_].soff = soff;
+        sl[rank_].sbytes = sbytes;
+        sl[rank_].ready = ready_[p];
+        sl[rank_].device = dev_;
+        if (g_->barrier(err)) return -1;
+        int rc = 0;
+        for (int r = 0; r < n_ && !rc; ++r) {
+            const uint64_t nb = sl[r].sbytes[rank_];
+            if (nb != rbytes[r]) {
+                err = "in-process exchange: rank " + std::to_string(r) + " sends " + std::to_string(nb) +
+                      " bytes, rank " + std::to_string(rank_) + " expects " + std::to_string(rbytes[r]);
+                rc = -1;
+                break;
+            }
+            if (!nb) continue;
+            hipError_t e = hipStreamWaitEvent(s, sl[r].ready, 0);
+            if (e == hipSuccess)
+                e = sl[r].device == dev_
+                        ? hipMemcpyAsync(recv + roff[r], sl[r].send + sl[r].soff[rank_], nb, hipMemcpyDeviceToDevice, s)
+                        : hipMemcpyPeerAsync(recv + roff[r], dev_, sl[r].send + sl[r].soff[rank_], sl[r].device, nb,
+                                             s);
+            if (e != hipSuccess) {
+                err = hip_msg("in-process exchange copy", e);
+                rc = -1;
+            }
+        }
+        if (rc) {
+            g_->fail();
+            return -1;
+        }
+        COMM_HIP(hipEventRecord(done_[p], s));
+        sl[rank_].done = done_[p];
+        if (g_->barrier(err)) return -1;
+        // this rank's send buffer stays untouched until every peer has copied out of it
+        for (int r = 0; r < n_; ++r)
+            if (r != rank_ && sbytes[r]) COMM_HIP(hipStreamWaitEvent(s, sl[r].done, 0));
+        return 0;
+    }
+
+    void abort() override { g_->fail(); }
+
+   private:
+    int next() { return (int)(seq_++ & 1u); }
+    std::shared_ptr<LocalGroup> g_;
+    int dev_;
+    uint64_t seq_ = 0;
+    hipEvent_t ready_[2] = {nullptr, nullptr}, done_[2] = {nullptr, nullptr};
+};
+
+}  // namespace
+
+int comm_unique_id(uint8_t id[COMM_ID_BYTES], std::string &err) {
+    const RcclApi *a = rccl(err);
+    if (!a) return -1;
+    ncclUniqueId u;
+    const ncclResult_t r = a->GetUniqueId(&u);
+    if (r != ncclSuccess) {
+        err = std::string("ncclGetUniqueId: ") + a->GetErrorString(r);
+        return -1;
+    }
+    memcpy(id, u.internal, COMM_ID_BYTES);
+    return 0;
+}
+
+Comm *comm_create_rccl(const uint8_t id[COMM_ID_BYTES], int n, int rank, int device, std::string &err) {
+    const RcclApi *a = rccl(err);
+    if (!a) return nullptr;
+    ncclUniqueId u;
+    memcpy(u.internal, id, COMM_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = a->CommInitRank(&comm, n, u, rank);  // blocks until every rank has joined
+    if (r != ncclSuccess) {
+        err = std::string("ncclCommInitRank: ") + a->GetErrorString(r);
+        return nullptr;
+    }
+    (void)device;
+    return new RcclComm(a, comm, n, rank);
+}
+
+int comm_create_local(int n, const int *devices, Comm **out, std::string &err) {
+    auto g = std::make_shared<LocalGroup>(n);
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    int rc = 0;
+    for (int r = 0; r < n; ++r) out[r] = nullptr;
+    for (int r = 0; r < n && !rc; ++r) {
+        if (hipSetDevice(devices[r]) != hipSuccess) {
+            err = "cannot select device " + std::to_string(devices[r]);
+            rc = -1;
+            break;
+        }
+        auto *c = new LocalComm(g, r, devices[r]);
+        rc = c->init(err);
+        out[r] = c;
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (rc)
+        for (int r = 0; r < n; ++r) {
+            delete out[r];
+            out[r] = nullptr;
+        }
+    return rc;
+}
+
+const char *comm_rccl_path() {
+    std::string ignore;
+    const RcclApi *a = rccl(ignore);
+    return a ? a->path.c_str() : "";
+}
+
+}  // namespace fk

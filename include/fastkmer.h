@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FK_ABI_VERSION 1
+#define FK_ABI_VERSION 2
 
 #define FK_OK 0
 #define FK_E_INVALID (-1) /* bad argument or configuration (reference: require / AIOOBE) */
@@ -76,6 +76,12 @@ typedef struct fk_stats {
                                   first header, 4 halo too short, 8 too many records in a tile (0: none) */
     uint64_t ht_spilled;       /* useHT LDS tables: keys the first round spilled (counted by later rounds) */
     uint64_t ht_rounds;        /* useHT LDS tables: rounds until every key was counted */
+    /* multi-rank exchange inside the context (fk_comm_init*), last fk_finish */
+    uint64_t xch_steps;        /* exchange steps (pieces sent during fk_ingest, the last piece, closing steps) */
+    uint64_t xch_bytes_sent;   /* record bytes sent to other ranks */
+    uint64_t xch_bytes_received; /* record bytes received from other ranks */
+    double ms_exchange;        /* sum over the steps of their record transfer time on the comm stream */
+    double ms_exchange_tail;   /* fk_finish: the last piece posted -> every rank's records received */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
@@ -164,6 +170,39 @@ int fk_finish(fk_ctx *ctx);
 int fk_map_bin_kmers(fk_ctx *ctx, uint64_t *kmers_per_bin);
 int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks, int32_t *owner);
 int fk_set_bin_owners(fk_ctx *ctx, const int32_t *owner, uint64_t *send_counts);
+
+/* ---- multi-GPU inside the context (one context per GPU) --------
+ * The job's contexts (fk_config.n_ranks = n, rank = 0..n-1) join one
+ * communicator.  A context then exchanges its records itself: fk_ingest
+ * groups every landed piece of its input (FASTKMER_PIECE_BYTES, 1 GB) by
+ * (owner rank, local bin) and sends it while the next piece is still being
+ * copied in; fk_finish sends the last piece, receives every rank's, and
+ * counts the bins this rank owns (bin % n_ranks), as the executors of the
+ * reference's reduceByKey shuffle do (SBKC:1034-1042).  fk_finish (and
+ * fk_ingest, which may send pieces) are collective: every rank of the job
+ * calls them, each from its own host thread or process.  Ranks may hold
+ * different amounts of input: a rank that has sent its last piece keeps
+ * answering the others' steps inside fk_finish. */
+#define FK_COMM_ID_BYTES 128
+/* A fresh RCCL unique id (ncclGetUniqueId): made on one rank, handed to all. */
+int fk_comm_unique_id(uint8_t id[FK_COMM_ID_BYTES]);
+/* RCCL over xGMI: joins the job's communicator (blocks until every rank has joined). */
+int fk_comm_init(fk_ctx *ctx, const uint8_t id[FK_COMM_ID_BYTES]);
+/* n contexts of this process as ranks 0..n-1 (created with n_ranks = n): records move
+ * by device-to-device copies; drive each context from its own host thread. */
+int fk_comm_init_local(fk_ctx **ctxs, int32_t n);
+/* "rccl", "local" or "" (no communicator). */
+const char *fk_comm_transport(const fk_ctx *ctx);
+/* Host-only arithmetic of one exchange step.  sent[d * (2 * parts + 1) + i] is this
+ * rank's message to rank d: records of local bin i (i < parts), k-mers of local bin
+ * i - parts, then a flag word (bit 0: the sender's last piece, bit 1: the sender
+ * retracts its earlier pieces); received[] holds every sender's message to this
+ * rank in the same layout.  Fills the byte offsets and sizes of the step's send
+ * blocks (records grouped by destination, rank 0 first) and receive blocks (by
+ * sender), and *all_final (every sender has sent its last piece). */
+int fk_exchange_plan(int32_t n_ranks, int32_t parts, const uint64_t *sent, const uint64_t *received,
+                     uint64_t record_bytes, uint64_t *send_off, uint64_t *send_bytes, uint64_t *recv_off,
+                     uint64_t *recv_bytes, int32_t *all_final);
 
 /* ---- results (device resident; copied out on request) ------------------ */
 

@@ -70,10 +70,41 @@ JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_ingest(JNIEnv *env, 
     if (rc != FK_OK) throw_fk(env, rc);
 }
 
-/* def finish(h): Unit -- map, count (one rank) */
+/* def finish(h): Unit -- map and count (one rank); with a communicator the last piece, the
+ * exchange with the other ranks and the count of this rank's bins (collective) */
 JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_finish(JNIEnv *env, jobject self, jlong h) {
     (void)self;
     const int rc = fk_finish(ctx_of(h));
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
+/* def commUniqueId(): Array[Byte] -- a fresh RCCL unique id, made on one executor (e.g. the
+ * driver) and handed to every rank of the job with the task closure */
+JNIEXPORT jbyteArray JNICALL Java_skc_gpu_NativeKmerCounter_00024_commUniqueId(JNIEnv *env, jobject self) {
+    (void)self;
+    uint8_t id[FK_COMM_ID_BYTES];
+    const int rc = fk_comm_unique_id(id);
+    if (rc != FK_OK) {
+        throw_fk(env, rc);
+        return NULL;
+    }
+    jbyteArray out = (*env)->NewByteArray(env, FK_COMM_ID_BYTES);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, FK_COMM_ID_BYTES, (const jbyte *)id);
+    return out;
+}
+
+/* def commInit(h, id: Array[Byte]): Unit -- join the job's RCCL communicator (every rank) */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_commInit(JNIEnv *env, jobject self, jlong h,
+                                                                    jbyteArray id) {
+    (void)self;
+    if (!id || (*env)->GetArrayLength(env, id) != FK_COMM_ID_BYTES) {
+        jclass ex = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+        if (ex) (*env)->ThrowNew(env, ex, "an RCCL unique id has 128 bytes");
+        return;
+    }
+    uint8_t buf[FK_COMM_ID_BYTES];
+    (*env)->GetByteArrayRegion(env, id, 0, FK_COMM_ID_BYTES, (jbyte *)buf);
+    const int rc = fk_comm_init(ctx_of(h), buf);
     if (rc != FK_OK) throw_fk(env, rc);
 }
 

@@ -23,6 +23,8 @@ object NativeKmerCounter {
                      nRanks: Int, rank: Int, device: Int): Long
   @native def ingest(h: Long, fasta: java.nio.ByteBuffer, n: Long, last: Boolean): Unit
   @native def finish(h: Long): Unit
+  @native def commUniqueId(): Array[Byte]
+  @native def commInit(h: Long, id: Array[Byte]): Unit
   @native def binSizes(h: Long): Array[Long]
   @native def writeBins(h: Long, outDir: String): Unit
   @native def findBinSignatures(h: Long, outDir: String): Unit
@@ -50,6 +52,28 @@ object NativeKmerCounter {
       ingestFile(h, configuration.dataset, window)
       finish(h)
       if (configuration.write) writeBins(h, configuration.outputDir)
+    } finally destroy(h)
+  }
+
+  /** One rank of an nRanks-GPU job (one executor per GPU): `commId` comes from commUniqueId()
+    * on one node and reaches every rank with the task (a broadcast variable); `split` is this
+    * rank's input -- (path, offset, length) of its byte range plus the k - 1 overlap, as the
+    * FASTdoop input splits of SBKC:1009-1012 cut it.  The records move between the GPUs inside
+    * finish (RCCL all-to-all over xGMI, the reduceByKey of :1034-1042); each rank writes the
+    * bin files of the bins it owns (bin % nRanks == rank) into the shared output directory. */
+  def executeJobRank(configuration: TestConfiguration, rank: Int, nRanks: Int, commId: Array[Byte],
+                     split: (String, Long, Long), device: Int = -1): Array[Long] = {
+    val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
+      configuration.useHT, configuration.sequenceType, nRanks, rank, device)
+    try {
+      commInit(h, commId)
+      val (path, off, len) = split
+      val ch = FileChannel.open(Paths.get(path), StandardOpenOption.READ)
+      try ingest(h, ch.map(FileChannel.MapMode.READ_ONLY, off, len), len, true)
+      finally ch.close()
+      finish(h)
+      if (configuration.write) writeBins(h, configuration.outputDir)
+      binSizes(h)
     } finally destroy(h)
   }
 

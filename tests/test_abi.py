@@ -32,7 +32,7 @@ def test_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert fk.lib().fk_abi_version() == 1
+    assert fk.lib().fk_abi_version() == 2
 
 
 @pytest.mark.parametrize("kw,ok", [

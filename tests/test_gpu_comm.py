@@ -1,0 +1,273 @@
+"""The multi-GPU job inside the library (fk_comm_*), through the C-ABI only.
+
+Each rank is one context; the contexts exchange their records themselves
+(grouped by owner rank = bin % n_ranks and local bin, one
+all-to-all-v per step -- the reduceByKey shuffle of SparkBinKmerCounter.scala
+:1034-1042 inside executeJob :989-1046), pieces of the input while later
+pieces are still being ingested, then each rank counts the bins it owns.
+No torch.distributed anywhere: the in-process transport (one host thread per
+context, device-to-device copies) runs the whole native path with many ranks
+on one GPU; the RCCL transport runs with one rank here (self send / receive)
+and with two where two GPUs exist.  Every result is compared with the CPU
+oracle on the whole input: the union of the ranks' bins must be bit-exact.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import fastkmer_amd as fk
+import oracle
+from test_gpu_parity import counter_arrays
+
+pytestmark = pytest.mark.gpu
+
+REC = 114
+
+
+def record_shards(fasta: bytes, world: int, rec_bytes: int = REC):
+    n = len(fasta) // rec_bytes
+    cuts = [r * n // world * rec_bytes for r in range(world + 1)]
+    return [fasta[cuts[r]:cuts[r + 1]] for r in range(world)]
+
+
+def run_local_job(shards, k, m, x=3, B=2048, use_ht=False, seq=0, feed="bytes", chunks=1):
+    """One context per shard joined in an in-process group; one thread per rank
+    ingests its shard (feed = bytes: pageable; pinned: a pinned host buffer)
+    and calls finish()."""
+    G = len(shards)
+    ctxs = [fk.KmerCounter(k, m, x, B, use_ht, seq, n_ranks=G, rank=r) for r in range(G)]
+    fk.comm_init_local(ctxs)
+    assert all(c.comm_transport == "local" for c in ctxs)
+    errs = [None] * G
+    keep = []
+    if feed == "pinned":
+        import torch
+        for sh in shards:
+            t = torch.empty(max(len(sh), 1), dtype=torch.uint8).pin_memory()
+            if sh:
+                t.numpy()[:len(sh)] = np.frombuffer(sh, dtype=np.uint8)
+            keep.append(t)
+
+    def work(r):
+        try:
+            sh = shards[r]
+            if feed == "pinned":
+                ctxs[r].ingest_ptr(keep[r].data_ptr(), len(sh))
+            elif chunks > 1:
+                cut = [len(sh) * i // chunks for i in range(chunks + 1)]
+                for i in range(chunks):
+                    ctxs[r].ingest_chunk(sh[cut[i]:cut[i + 1]], i == chunks - 1)
+            else:
+                ctxs[r].ingest(sh)
+            ctxs[r].finish()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs[r] = e
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank did not finish"
+    for e in errs:
+        if e is not None:
+            raise e
+    return ctxs
+
+
+def assert_union_matches_oracle(ctxs, ref, ordered=True):
+    G = len(ctxs)
+    ref_sizes = ref.bin_sizes()
+    total = np.zeros(ref.nbins, dtype=np.int64)
+    for r, kc in enumerate(ctxs):
+        sizes = kc.bin_sizes().astype(np.int64)
+        own = np.arange(ref.nbins) % G == r
+        assert np.all(sizes[~own] == 0), f"rank {r} holds bins it does not own"
+        total += sizes
+    bad = np.nonzero(total != ref_sizes)[0]
+    assert len(bad) == 0, f"bin sizes differ in {len(bad)} bins, e.g. {bad[:5]}"
+    for b in np.nonzero(ref_sizes)[0].tolist():
+        hi, lo, cnt = counter_arrays(ctxs[b % G], b)
+        rhi, rlo, rcnt = ref.bin_arrays(b)
+        if not ordered:
+            order = np.lexsort((lo, hi))
+            hi, lo, cnt = hi[order], lo[order], cnt[order]
+        assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo), f"keys differ in bin {b}"
+        assert np.array_equal(cnt, rcnt), f"counts differ in bin {b}"
+
+
+@pytest.fixture
+def small_pieces(monkeypatch):
+    # 256 KB H2D segments and 512 KB pieces: a few MB of input crosses several pieces
+    monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
+
+
+@pytest.mark.parametrize("world,use_ht,feed", [(2, False, "pinned"), (3, False, "bytes"), (8, False, "pinned"),
+                                              (2, True, "pinned"), (5, True, "bytes")])
+def test_local_exchange_vs_oracle(small_pieces, world, use_ht, feed):
+    fasta = fk.synth_fasta(40_000, 100, 1_000_000, seed=0xE1 + world)
+    ctxs = run_local_job(record_shards(fasta, world), 28, 10, 3, 2048, use_ht, feed=feed)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    st = [c.stats() for c in ctxs]
+    assert sum(s["kmers"] for s in st) == ref.total_kmers
+    if feed == "pinned":  # pieces went out during the ingest, then the last piece (and closing steps)
+        assert all(s["xch_steps"] >= (3 if world == 2 else 2) for s in st)
+    assert sum(s["xch_bytes_sent"] for s in st) == sum(s["xch_bytes_received"] for s in st) > 0
+    assert_union_matches_oracle(ctxs, ref, ordered=not use_ht)
+
+
+def test_local_exchange_streamed_chunks(small_pieces):
+    # several fk_ingest calls per rank (last = 0 ... 1): pieces cut across call boundaries
+    fasta = fk.synth_fasta(30_000, 100, 500_000, seed=0xE7)
+    ctxs = run_local_job(record_shards(fasta, 3), 28, 10, 3, 2048, chunks=5)
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 2048))
+
+
+def test_local_exchange_uneven_and_empty_ranks(small_pieces):
+    # ranks with very different inputs (and one with none) take different numbers of
+    # steps; the finished ranks answer the others' steps until every rank is done
+    fasta = fk.synth_fasta(36_000, 100, 800_000, seed=0xE2)
+    n = len(fasta) // REC
+    cuts = [0, n * 2 // 3, n * 2 // 3, n * 5 // 6, n]
+    shards = [fasta[cuts[i] * REC:cuts[i + 1] * REC] for i in range(4)]
+    assert shards[1] == b""
+    ctxs = run_local_job(shards, 28, 10, 3, 2048, feed="pinned")
+    steps = [c.stats()["xch_steps"] for c in ctxs]
+    assert len(set(steps)) == 1  # every rank took part in every step
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 2048))
+
+
+def test_local_exchange_retracts_pieces_on_fallback(small_pieces):
+    # a 40 KB header line late in rank 0's input (a tile starts more than the 4 KB read-back
+    # inside it) makes the fused map hand the input back
+    # after pieces were sent: rank 0 maps again from scratch, retracts its earlier
+    # pieces and sends everything with its last piece
+    fasta = fk.synth_fasta(30_000, 100, 600_000, seed=0xE3)
+    shards = record_shards(fasta, 2)
+    cut = len(shards[0]) * 7 // 8 // REC * REC
+    long_header = b">" + b"h" * 40_000 + b"\n" + b"ACGT" * 30 + b"\n"
+    shards[0] = shards[0][:cut] + long_header + shards[0][cut:]
+    ctxs = run_local_job(shards, 28, 10, 3, 2048, feed="pinned")
+    assert ctxs[0].stats()["fused_map"] == 0
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(shards[0] + shards[1], 28, 10, 2048))
+
+
+def test_local_exchange_configs2_shape(small_pieces):
+    # BASELINE configs[2] parameters: k=28 m=10 x=3 B=8192 over 8 ranks
+    fasta = fk.synth_fasta(48_000, 100, 2_000_000, seed=0xC3)
+    ctxs = run_local_job(record_shards(fasta, 8), 28, 10, 3, 8192, feed="pinned")
+    assert all(c.num_bins == 8192 for c in ctxs)
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 8192))
+
+
+@pytest.mark.parametrize("use_ht", [False, True])
+def test_local_exchange_two_word_k55(small_pieces, use_ht):
+    # BASELINE configs[3] parameters: k=55 m=12 x=3 B=8192, 150 bp reads, 24-byte records
+    fasta = fk.synth_fasta(12_000, 150, 1_000_000, seed=0xC4)
+    ctxs = run_local_job(record_shards(fasta, 4, 164), 55, 12, 3, 8192, use_ht, feed="pinned")
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 55, 12, 8192), ordered=not use_ht)
+
+
+def test_local_exchange_long_sequence(small_pieces, tmp_path):
+    # sequenceType = 1: one record cut into byte ranges with the k - 1 overlap (sharding.read_shard)
+    from fastkmer_amd.sharding import read_shard
+    rng = np.random.default_rng(9)
+    seq = np.frombuffer(b"ACGTN", dtype=np.uint8)[rng.choice(5, 3_000_000, p=[.245, .245, .245, .245, .02])]
+    lines = b"\n".join(seq[i:i + 60].tobytes() for i in range(0, len(seq), 60))
+    fasta = b">chr1 synthetic\n" + lines + b"\n"
+    path = tmp_path / "long.fa"
+    path.write_bytes(fasta)
+    shards = [read_shard(str(path), 3, r, 28).piece for r in range(3)]
+    ctxs = run_local_job(shards, 28, 10, 3, 2048, seq=1, feed="pinned")
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 2048, sequence_type=1))
+
+
+def test_local_exchange_device_input_and_reuse(small_pieces):
+    # the same contexts run two jobs: device-resident inputs (one step each), then host inputs
+    import torch
+    fasta = fk.synth_fasta(20_000, 100, 400_000, seed=0xE4)
+    shards = record_shards(fasta, 2)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    ctxs = [fk.KmerCounter(28, 10, 3, 2048, n_ranks=2, rank=r) for r in range(2)]
+    fk.comm_init_local(ctxs)
+    dev = [torch.frombuffer(bytearray(sh), dtype=torch.uint8).cuda() for sh in shards]
+    torch.cuda.synchronize()
+    for job in range(2):
+        errs = [None, None]
+
+        def work(r):
+            try:
+                if job == 0:
+                    ctxs[r].ingest_device(dev[r].data_ptr(), dev[r].numel())
+                else:
+                    ctxs[r].ingest(shards[r])
+                ctxs[r].finish()
+            except Exception as e:  # noqa: BLE001
+                errs[r] = e
+        th = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+        [t.start() for t in th]
+        [t.join(timeout=300) for t in th]
+        assert errs == [None, None], errs
+        assert_union_matches_oracle(ctxs, ref)
+
+
+def test_rccl_single_rank_self_exchange(small_pieces):
+    # the RCCL transport end to end with one rank (self send / receive): comm init from a
+    # unique id, the pieced ingest, the count
+    import torch
+    fasta = fk.synth_fasta(30_000, 100, 600_000, seed=0xE5)
+    host = torch.empty(len(fasta), dtype=torch.uint8).pin_memory()
+    host.numpy()[:] = np.frombuffer(fasta, dtype=np.uint8)
+    with fk.KmerCounter(28, 10, 3, 2048, n_ranks=1, rank=0) as kc:
+        kc.comm_init(fk.comm_unique_id())
+        assert kc.comm_transport == "rccl"
+        for _ in range(2):
+            kc.ingest_ptr(host.data_ptr(), len(fasta))
+            kc.finish()
+            st = kc.stats()
+            assert st["xch_steps"] >= 3 and st["records_received"] == st["superkmers"]
+            ref = oracle.OracleResult(fasta, 28, 10, 2048)
+            assert_union_matches_oracle([kc], ref)
+
+
+def _rccl_rank(rank, world, uid, path, out_dir, q):
+    try:
+        import torch  # noqa: F401  (one HIP runtime per process, see fastkmer_amd.lib)
+        import fastkmer_amd as fk_
+        from fastkmer_amd.sharding import read_shard
+        piece = read_shard(path, world, rank, 28).piece
+        with fk_.KmerCounter(28, 10, 3, 2048, n_ranks=world, rank=rank, device=rank) as kc:
+            kc.comm_init(uid)
+            kc.ingest(piece)
+            kc.finish()
+            kc.write_bins(out_dir)
+            q.put((rank, kc.stats()["xch_bytes_sent"], None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, 0, repr(e)))
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() < 2, reason="RCCL between ranks needs two GPUs")
+def test_rccl_two_ranks_write_bins(tmp_path):
+    import multiprocessing as mp
+    fasta = fk.synth_fasta(30_000, 100, 600_000, seed=0xE6)
+    path = tmp_path / "in.fa"
+    path.write_bytes(fasta)
+    out = tmp_path / "out"
+    uid = fk.comm_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rccl_rank, args=(r, 2, uid, str(path), str(out), q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = [q.get(timeout=300) for _ in range(2)]
+    [p.join(timeout=60) for p in ps]
+    assert all(e is None for _, _, e in res), res
+    assert all(sent > 0 for _, sent, _ in res)
+    ref_dir = tmp_path / "ref"
+    oracle.OracleResult(fasta, 28, 10, 2048).write_bins(str(ref_dir))
+    files = sorted(os.listdir(ref_dir))
+    assert sorted(os.listdir(out)) == files
+    for f in files:
+        assert (out / f).read_bytes() == (ref_dir / f).read_bytes(), f
