@@ -294,16 +294,35 @@ struct fk_ctx {
     // is emitted in pieces grouped by (destination, local bin) and each piece is exchanged
     // while the next one is still being copied in; fk_finish sends the last piece, then
     // counts every received segment (the reduceByKey shuffle of SBKC:1034-1042)
+    // per-piece counts (sorted count): pieces are counted while later ones are still being copied
+    // in (or received), fk_finish counts the last one and merges the pieces' results (fk_merge.inc)
+    struct PieceRes {
+        DevBuf keys, counts, bin_off;
+        std::vector<uint64_t> h_bin_off;
+        uint64_t distinct = 0;
+    };
+    PieceRes acc, acc2, tmp;      // running result of the counted pieces, merge target, the newest piece
+    uint32_t npieces = 0;         // pieces counted into acc in the current job
+    bool pieces_void = false;     // a fallback or a retract: the pieces are counted again at the end
+    bool count_pieces = true;     // FASTKMER_PIECE_COUNT=0: count the whole input in fk_finish
+    uint64_t tiles_counted = 0;   // one rank: tiled records [0, tiles_counted) counted
+    size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) counted
+    double acc_ms_part = 0.0, acc_ms_count = 0.0, acc_ms_merge = 0.0;  // the job's earlier pieces
+    DevBuf m2_tile_bin, m2_bin_tile0, m2_split_a, m2_split_b, m2_bnd, m2_tcount, m2_toff, m2_keys, m2_counts;
+
     fk::Comm *comm = nullptr;
     hipStream_t comm_stream = nullptr;
     hipEvent_t emit_ev = nullptr;                // map stream: a piece's send records are written
     std::vector<hipEvent_t> xev;                 // comm stream: begin / end of every piece's transfer
-    uint64_t piece_bytes = 1ull << 30;           // FASTKMER_PIECE_BYTES: FASTA bytes per piece
+    uint64_t piece_bytes = 512ull << 20;         // FASTKMER_PIECE_BYTES: FASTA bytes per piece (1 GB with a
+                                                 // communicator)
+    bool piece_bytes_set = false;
     uint64_t ingest_seg = 32ull << 20;           // FASTKMER_INGEST_SEG: H2D segment of a pinned source
     DevBuf xsend, xrecv;                         // send ring (pieces in flight), received records
     struct XSeg {                                // received records of one (piece, sender)
         uint64_t off;                            // first record in xrecv
         int32_t sender;
+        uint64_t step;                           // the exchange step that delivered it
         std::vector<uint64_t> rec, kmer;         // per local bin
     };
     struct Xch {
@@ -459,8 +478,11 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (lh && lh[0]) c->lh_mode = atoi(lh);
     const char *lp = getenv("FASTKMER_LH_PROBE");
     if (lp && lp[0]) c->lh_probe = atoi(lp);
-    if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0])
+    if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
+        c->piece_bytes_set = true;
+    }
+    if (const char *pc = getenv("FASTKMER_PIECE_COUNT"); pc && pc[0]) c->count_pieces = atoi(pc) != 0;
     if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
         c->ingest_seg = std::max(1ull << 16, strtoull(sg, nullptr, 10));
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -532,6 +554,11 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->comm = nullptr;
     release(c->xsend);
     release(c->xrecv);
+    for (fk_ctx::PieceRes *r : {&c->acc, &c->acc2, &c->tmp})
+        for (DevBuf *b : {&r->keys, &r->counts, &r->bin_off}) release(*b);
+    for (DevBuf *b : {&c->m2_tile_bin, &c->m2_bin_tile0, &c->m2_split_a, &c->m2_split_b, &c->m2_bnd, &c->m2_tcount,
+                      &c->m2_toff, &c->m2_keys, &c->m2_counts})
+        release(*b);
     for (auto &e : c->xev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : c->seg_evs)
@@ -627,7 +654,9 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
 }
 
 static int xch_maybe_piece(fk_ctx *c);
+static int local_maybe_piece(fk_ctx *c);
 static void xch_reset(fk_ctx *c);
+static void pieces_reset(fk_ctx *c);
 
 // Appends host bytes to the device input on the copy stream, in segments.
 // Pinned sources are copied by DMA directly; pageable ones through two
@@ -657,6 +686,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
             xch_reset(c);
         }
         HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
+        pieces_reset(c);
         c->pm_active = premap_eligible(c);
         c->pm_tiles = 0;
         c->pm_last_seen = false;
@@ -721,6 +751,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
             HIP_TRY(hipStreamWaitEvent(s, c->seg_evs[i], 0));
             FK_TRY(premap_launch(c, have + off, last && off == n));
             if (pieces) FK_TRY(xch_maybe_piece(c));
+            else if (c->pm_active) FK_TRY(local_maybe_piece(c));
         }
     } else {
         size_t off = 0;
@@ -736,6 +767,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
                 HIP_TRY(hipStreamWaitEvent(s, c->seg_ev, 0));
                 FK_TRY(premap_launch(c, have + off, last && off == n));
                 if (pieces) FK_TRY(xch_maybe_piece(c));
+                else FK_TRY(local_maybe_piece(c));
             }
         }
         HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
@@ -774,6 +806,7 @@ FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
     c->dev_open = last == 0;  // a borrowed input takes no appended host chunks
     c->ingest_fresh = true;
     c->pm_active = false;
+    pieces_reset(c);
     reset_results(c);
     if (((uintptr_t)d & 15) != 0) {
         FK_TRY(ensure(c->fasta_own, n));
@@ -810,6 +843,7 @@ FK_EXPORT int fk_synth_fasta_device(fk_ctx *c, uint64_t first_read, uint64_t n_r
     c->dev_open = false;
     c->ingest_fresh = true;
     c->pm_active = false;
+    pieces_reset(c);
     c->d_fasta = c->fasta_own.as<uint8_t>();
     c->n_fasta = nb;
     reset_results(c);
@@ -1619,7 +1653,7 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
 
 // reduce of the records of `src` (all owned by this rank): partition by local bin, then count
 static int reduce_src(fk_ctx *c, const RecSrc &src) {
-    const uint64_t nrecv = src.nrec;
+    uint64_t nrecv = src.nrec;  // tiled sources: an upper bound, the partition counts them
     const double t0 = now_ms();
     hipStream_t s = c->stream;
     c->have_result = false;
@@ -1639,6 +1673,7 @@ static int reduce_src(fk_ctx *c, const RecSrc &src) {
         ranges[lb].push_back({off, off + brec[lb]});
         off += brec[lb];
     }
+    if (src.tcnt) nrecv = off;
     if (off != nrecv)
         return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
                        (unsigned long long)off, (unsigned long long)nrecv);
@@ -1732,6 +1767,164 @@ FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, c
         return set_err(FK_E_INVALID, "segment table holds %llu records, buffer %llu", (unsigned long long)off,
                        (unsigned long long)nrecv);
     return reduce_ranges(c, (const uint64_t *)d_recv, nrecv, ranges, bkm, t0);
+}
+
+// ---------------------------------------------------------------------------
+// per-piece counts and their merge (fk_merge.inc)
+// ---------------------------------------------------------------------------
+
+static void pieces_reset(fk_ctx *c) {
+    c->npieces = 0;
+    c->pieces_void = false;
+    c->tiles_counted = 0;
+    c->segs_counted = 0;
+    c->acc_ms_part = c->acc_ms_count = c->acc_ms_merge = 0.0;
+}
+
+// Pieces are counted separately for the sorted count (its results merge in key order); the hash
+// count's table order does not, it counts the whole input at the end.
+static bool piece_counting(const fk_ctx *c) { return c->count_pieces && !c->pieces_void && !c->cfg.use_ht; }
+
+static void swap_result(fk_ctx *c, fk_ctx::PieceRes &r) {
+    std::swap(r.keys, c->dense_keys);
+    std::swap(r.counts, c->dense_counts);
+    std::swap(r.bin_off, c->bin_off);
+    r.h_bin_off.swap(c->h_bin_off);
+    std::swap(r.distinct, c->distinct);
+}
+
+static void swap_res(fk_ctx::PieceRes &a, fk_ctx::PieceRes &b) {
+    std::swap(a.keys, b.keys);
+    std::swap(a.counts, b.counts);
+    std::swap(a.bin_off, b.bin_off);
+    a.h_bin_off.swap(b.h_bin_off);
+    std::swap(a.distinct, b.distinct);
+}
+
+static MergeSrc merge_src(const DevBuf &keys, const DevBuf &counts, const DevBuf &bin_off) {
+    MergeSrc m;
+    m.keys = keys.as<uint64_t>();
+    m.counts = counts.as<uint32_t>();
+    m.bin_off = bin_off.as<uint64_t>();
+    return m;
+}
+
+// out = the per-bin union of results a and b (fk_merge.inc).
+static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &b, DevBuf &okeys, DevBuf &ocounts,
+                  DevBuf &obin_off, std::vector<uint64_t> &oh_bin_off, uint64_t *odistinct) {
+    hipStream_t s = c->stream;
+    const uint32_t nlb = c->nlb;
+    const double t0 = now_ms();
+    std::vector<uint32_t> tile_bin, bin_tile0(nlb);
+    tile_bin.reserve((a.distinct + b.distinct) / MERGE_TILE + nlb + 1);
+    for (uint32_t lb = 0; lb < nlb; ++lb) {
+        const uint64_t n = a.h_bin_off[lb + 1] - a.h_bin_off[lb] + b.h_bin_off[lb + 1] - b.h_bin_off[lb];
+        const uint64_t nt = std::max<uint64_t>(1, (n + MERGE_TILE - 1) / MERGE_TILE);
+        bin_tile0[lb] = (uint32_t)tile_bin.size();
+        tile_bin.insert(tile_bin.end(), nt, lb);
+    }
+    const uint64_t ntiles = tile_bin.size();
+    if (!ntiles) {  // no local bins
+        oh_bin_off.assign(1, 0);
+        *odistinct = 0;
+        FK_TRY(ensure(obin_off, 8));
+        HIP_TRY(hipMemsetAsync(obin_off.p, 0, 8, s));
+        return FK_OK;
+    }
+    HIP_TRY(hipEventRecord(c->ev[6], s));
+    FK_TRY(ensure(c->m2_tile_bin, ntiles * 4));
+    FK_TRY(ensure(c->m2_bin_tile0, (uint64_t)nlb * 4));
+    FK_TRY(ensure(c->m2_split_a, (ntiles + 1) * 8));
+    FK_TRY(ensure(c->m2_split_b, (ntiles + 1) * 8));
+    FK_TRY(ensure(c->m2_bnd, (ntiles + 1) * 8));
+    FK_TRY(ensure(c->m2_tcount, ntiles * 4));
+    FK_TRY(ensure(c->m2_toff, (ntiles + 1) * 8));
+    FK_TRY(ensure(c->m2_keys, ntiles * MERGE_TILE * 8 * c->KW));
+    FK_TRY(ensure(c->m2_counts, ntiles * MERGE_TILE * 4));
+    HIP_TRY(hipMemcpyAsync(c->m2_tile_bin.p, tile_bin.data(), ntiles * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->m2_bin_tile0.p, bin_tile0.data(), (uint64_t)nlb * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_merge2(c->KW, merge_src(a.keys, a.counts, a.bin_off), merge_src(b.keys, b.counts, b.bin_off),
+                          c->m2_tile_bin.as<uint32_t>(), c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles,
+                          c->m2_split_a.as<uint64_t>(), c->m2_split_b.as<uint64_t>(), c->m2_bnd.as<uint64_t>(),
+                          c->m2_tcount.as<uint32_t>(), c->m2_keys.as<uint64_t>(), c->m2_counts.as<uint32_t>(), s));
+    HIP_TRY(scan_excl_sum_u32_to_u64(c->m2_tcount.as<uint32_t>(), c->m2_toff.as<uint64_t>(), ntiles,
+                                     c->m2_toff.as<uint64_t>() + ntiles, c->ws, s));
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, c->m2_toff.as<uint64_t>() + ntiles, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    FK_TRY(ensure(okeys, total * 8 * c->KW));
+    FK_TRY(ensure(ocounts, total * 4));
+    FK_TRY(ensure(obin_off, ((uint64_t)nlb + 1) * 8));
+    HIP_TRY(launch_merge2_pack(c->KW, c->m2_tcount.as<uint32_t>(), c->m2_toff.as<uint64_t>(),
+                               c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles, c->m2_keys.as<uint64_t>(),
+                               c->m2_counts.as<uint32_t>(), okeys.as<uint64_t>(), ocounts.as<uint32_t>(),
+                               obin_off.as<uint64_t>(), s));
+    HIP_TRY(hipEventRecord(c->ev[7], s));
+    oh_bin_off.assign((size_t)nlb + 1, 0);
+    HIP_TRY(hipMemcpyAsync(oh_bin_off.data(), obin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *odistinct = oh_bin_off[nlb];
+    c->acc_ms_merge += ev_ms(c->ev[6], c->ev[7]);
+    c->stats.ms_total += now_ms() - t0;
+    return FK_OK;
+}
+
+// Counts one piece (`count` writes the context's result buffers; the piece slot's buffers stand
+// in for them meanwhile) and merges it into the running result.  With `last`, the merge goes to
+// the context's result buffers: the job's result.
+template <class F>
+static int count_piece(fk_ctx *c, F count, bool last) {
+    swap_result(c, c->tmp);
+    const int rc = count();
+    swap_result(c, c->tmp);
+    if (rc) return rc;
+    c->acc_ms_part += c->stats.ms_partition;
+    c->acc_ms_count += c->stats.ms_count;
+    c->have_result = false;
+    if (c->npieces == 0) {
+        if (last) swap_result(c, c->tmp);
+        else swap_res(c->acc, c->tmp);
+    } else if (!last) {
+        FK_TRY(merge2(c, c->acc, c->tmp, c->acc2.keys, c->acc2.counts, c->acc2.bin_off, c->acc2.h_bin_off,
+                      &c->acc2.distinct));
+        swap_res(c->acc, c->acc2);
+    } else {
+        FK_TRY(merge2(c, c->acc, c->tmp, c->dense_keys, c->dense_counts, c->bin_off, c->h_bin_off, &c->distinct));
+    }
+    c->npieces += 1;
+    return FK_OK;
+}
+
+// The job's result from the counted pieces: the last merge wrote it, or one piece is all there is.
+static void finish_pieces(fk_ctx *c, bool merged_last) {
+    if (!merged_last) swap_result(c, c->acc);
+    c->stats.ms_partition = c->acc_ms_part;
+    c->stats.ms_count = c->acc_ms_count;
+    c->stats.ms_merge = c->acc_ms_merge;
+    c->stats.pieces_counted = c->npieces;
+    c->stats.distinct = c->distinct;
+    c->have_result = true;
+}
+
+// One rank: counts the tiles mapped since the last piece once they cover a piece (fk_ingest).
+// The fused map's fallback flag is read first: a flagged input is counted whole by fk_finish.
+static int local_maybe_piece(fk_ctx *c) {
+    if (!piece_counting(c)) return FK_OK;
+    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    if ((c->pm_tiles - c->tiles_counted) * tile < c->piece_bytes) return FK_OK;
+    uint64_t h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[2]) {
+        c->pieces_void = true;
+        return FK_OK;
+    }
+    const uint64_t t0 = c->tiles_counted, nt = c->pm_tiles - t0;
+    const uint32_t tcap = map_fused_tcap();
+    const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
+                                 nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
+    c->tiles_counted = c->pm_tiles;
+    return count_piece(c, [&] { return reduce_src(c, src); }, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -1873,6 +2066,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
     for (uint32_t r = 0; r < G; ++r) {
         const uint64_t *m = in.data() + (size_t)r * msg;
         if (m[2 * L] & XF_RETRACT) {  // the sender mapped again from scratch: its earlier pieces are void
+            c->pieces_void = true;      // (and so are the piece counts that hold them)
             auto &v = c->xch.segs;
             v.erase(std::remove_if(v.begin(), v.end(), [&](const fk_ctx::XSeg &g) { return g.sender == (int32_t)r; }),
                     v.end());
@@ -1881,6 +2075,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
         fk_ctx::XSeg g;
         g.off = c->xch.recv_used + roff[r] / rb;
         g.sender = (int32_t)r;
+        g.step = step;
         g.rec.assign(m, m + L);
         g.kmer.assign(m + L, m + 2 * L);
         c->xch.segs.push_back(std::move(g));
@@ -1895,6 +2090,46 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
     c->xch.all_final = all_final;
     if (flags & XF_FINAL) c->xch.sent_final = true;
     return FK_OK;
+}
+
+// Ranges of every local bin over the received segments [s0, s1) (each segment holds its
+// records bin after bin).
+static int segment_ranges(fk_ctx *c, size_t s0, size_t s1, std::vector<std::vector<std::pair<uint64_t, uint64_t>>> &ranges,
+                          std::vector<uint64_t> &bkm, uint64_t *nrecv) {
+    const uint32_t nlb = c->nlb;
+    ranges.assign(nlb, {});
+    bkm.assign(nlb, 0);
+    *nrecv = 0;
+    for (size_t i = s0; i < s1; ++i) {
+        const fk_ctx::XSeg &g = c->xch.segs[i];
+        uint64_t off = g.off;
+        for (uint32_t lb = 0; lb < c->grp_nlb; ++lb) {
+            const uint64_t n = g.rec[lb];
+            if (n && lb >= nlb) return set_err(FK_E_INVALID, "records for local bin %u of %u", lb, nlb);
+            if (n) {
+                ranges[lb].push_back({off, off + n});
+                bkm[lb] += g.kmer[lb];
+                *nrecv += n;
+            }
+            off += n;
+        }
+    }
+    return FK_OK;
+}
+
+// Counts the received segments [segs_counted, s1) as one piece result, once the comm stream has
+// delivered them (the end event of the step of the last one).
+static int xch_count_segments(fk_ctx *c, size_t s1, bool last) {
+    if (s1 <= c->segs_counted) return FK_OK;
+    const uint64_t step = c->xch.segs[s1 - 1].step;
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->xev[2 * step + 1], 0));
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges;
+    std::vector<uint64_t> bkm;
+    uint64_t nrecv = 0;
+    FK_TRY(segment_ranges(c, c->segs_counted, s1, ranges, bkm, &nrecv));
+    c->segs_counted = s1;
+    return count_piece(c, [&] { return reduce_ranges(c, c->xrecv.as<uint64_t>(), nrecv, ranges, bkm, now_ms()); },
+                       last);
 }
 
 // fk_ingest: sends the tiles mapped since the last piece once they cover a piece.  The fused
@@ -1916,8 +2151,12 @@ static int xch_maybe_piece(fk_ctx *c) {
     const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
                                  nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
     c->xch.tiles_sent = c->pm_tiles;
+    const size_t before = c->xch.segs.size();
     const int rc = xch_step(c, &src, 0);
-    return rc ? comm_fail(c, rc) : FK_OK;
+    if (rc) return comm_fail(c, rc);
+    // the records of the earlier steps are counted while this step's are on the wire
+    if (piece_counting(c) && before > c->segs_counted) FK_TRY(xch_count_segments(c, before, false));
+    return FK_OK;
 }
 
 // fk_finish with a communicator: the last piece, the closing steps, then the count of every
@@ -1946,25 +2185,21 @@ static int finish_exchange(fk_ctx *c) {
     if (rc) return comm_fail(c, rc);
     HIP_TRY(hipEventRecord(c->ev[4], cs));  // every rank's records have landed
     HIP_TRY(hipStreamWaitEvent(s, c->ev[4], 0));
-    // segments, bin after bin inside each: the ranges of every local bin
-    const uint32_t nlb = c->nlb;
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
-    std::vector<uint64_t> bkm(nlb, 0);
     uint64_t nrecv = 0;
-    for (const auto &g : c->xch.segs) {
-        uint64_t off = g.off;
-        for (uint32_t lb = 0; lb < c->grp_nlb; ++lb) {
-            const uint64_t n = g.rec[lb];
-            if (n && lb >= nlb) return set_err(FK_E_INVALID, "records for local bin %u of %u", lb, nlb);
-            if (n) {
-                ranges[lb].push_back({off, off + n});
-                bkm[lb] += g.kmer[lb];
-                nrecv += n;
-            }
-            off += n;
-        }
+    for (const auto &g : c->xch.segs)
+        for (uint64_t n : g.rec) nrecv += n;
+    if (c->npieces && !c->pieces_void) {
+        // earlier steps were counted while later ones were on the wire: the rest, merged in
+        const bool more = c->segs_counted < c->xch.segs.size();
+        if (more) FK_TRY(xch_count_segments(c, c->xch.segs.size(), true));
+        finish_pieces(c, more);
+    } else {
+        std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges;
+        std::vector<uint64_t> bkm;
+        FK_TRY(segment_ranges(c, 0, c->xch.segs.size(), ranges, bkm, &nrecv));
+        FK_TRY(reduce_ranges(c, c->xrecv.as<uint64_t>(), nrecv, ranges, bkm, t0));
     }
-    FK_TRY(reduce_ranges(c, c->xrecv.as<uint64_t>(), nrecv, ranges, bkm, t0));
+    pieces_reset(c);
     // exchange figures (every transfer has completed: the count waited for them)
     double ms = 0.0;
     for (size_t i = 0; i < (size_t)c->xch.pieces; ++i) ms += ev_ms(c->xev[2 * i], c->xev[2 * i + 1]);
@@ -1989,6 +2224,22 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
                                    "fk_map/fk_map_emit/fk_reduce", c->G);
     FK_TRY(fk_map(c, nullptr));
     DeviceGuard dg_(c->device);
+    if (c->npieces && c->rec_tiled && !c->pieces_void && c->tiles_counted <= c->rec_tiles) {
+        // pieces were counted while the input landed: the last piece, merged in
+        const bool more = c->rec_tiles > c->tiles_counted;
+        if (more) {
+            const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
+            const uint32_t tcap = map_fused_tcap();
+            const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
+                                         nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
+            FK_TRY(count_piece(c, [&] { return reduce_src(c, src); }, true));
+        }
+        finish_pieces(c, more);
+        c->stats.records_received = c->nrec;
+        pieces_reset(c);
+        return FK_OK;
+    }
+    pieces_reset(c);
     return reduce_src(c, map_src(c));
 }
 
@@ -1997,6 +2248,7 @@ static int attach_comm(fk_ctx *c, fk::Comm *comm) {
     if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     if (!c->emit_ev) HIP_TRY(hipEventCreateWithFlags(&c->emit_ev, hipEventDisableTiming));
     c->comm = comm;
+    if (!c->piece_bytes_set) c->piece_bytes = 1ull << 30;
     FK_TRY(fk_set_grouped_emit(c, 1));  // records leave grouped by (owner rank, local bin)
     xch_reset(c);
     return FK_OK;

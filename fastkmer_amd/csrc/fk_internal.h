@@ -226,6 +226,25 @@ hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, 
 hipError_t launch_ht_gather(const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb, const uint64_t *okeys,
                             const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt, hipStream_t s);
 
+// ---- merge of two count results (fk_merge.inc): the per-bin union, equal k-mers' counts added
+struct MergeSrc {          // one result
+    const uint64_t *keys;     // KW words per entry, ascending per bin
+    const uint32_t *counts;
+    const uint64_t *bin_off;  // [nlb + 1]
+};
+constexpr uint32_t MERGE_TILE = 1024;  // merged entries per workgroup (M2_TILE)
+// tile_bin[ntiles]: the bin of every tile (each bin has ceil((na + nb) / MERGE_TILE) >= 1 tiles, in
+// bin order), bin_tile0[nlb]: its first tile; split_a / split_b / bnd: ntiles + 1 u64; tcount: ntiles;
+// sparse keys / counts: ntiles * MERGE_TILE entries (every tile's slot)
+hipError_t launch_merge2(int KW, const MergeSrc &A, const MergeSrc &B, const uint32_t *tile_bin,
+                         const uint32_t *bin_tile0, uint32_t nlb, uint64_t ntiles, uint64_t *split_a, uint64_t *split_b,
+                         uint64_t *bnd, uint32_t *tcount, uint64_t *sparse_keys, uint32_t *sparse_counts,
+                         hipStream_t s);
+// toff = exclusive scan of tcount (ntiles + 1): the dense result and its bin offsets (nlb + 1)
+hipError_t launch_merge2_pack(int KW, const uint32_t *tcount, const uint64_t *toff, const uint32_t *bin_tile0,
+                              uint32_t nlb, uint64_t ntiles, const uint64_t *sparse_keys, const uint32_t *sparse_counts,
+                              uint64_t *out_keys, uint32_t *out_counts, uint64_t *bin_off, hipStream_t s);
+
 // ---- synthetic input
 hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);
 

@@ -82,6 +82,9 @@ typedef struct fk_stats {
     uint64_t xch_bytes_received; /* record bytes received from other ranks */
     double ms_exchange;        /* sum over the steps of their record transfer time on the comm stream */
     double ms_exchange_tail;   /* fk_finish: the last piece posted -> every rank's records received */
+    /* pieces counted while later ones were still being copied in / received (sorted count) */
+    uint64_t pieces_counted;   /* piece results merged by the last fk_finish (0: one count of the whole input) */
+    double ms_merge;           /* their k-way merge (k_merge_plan / k_merge_segments / k_merge_compact) */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

@@ -1,0 +1,105 @@
+"""Per-piece counts merged into a running result (fk_merge.inc), through the C-ABI.
+
+While the FASTA is still being copied in, every landed piece of it is
+counted on its own (the sorted count of extractKXmers, SBKC:540-597, on the
+piece's records) and merged into the running result of the earlier pieces
+bin by bin, adding the counts of equal k-mers; fk_finish counts and merges
+the last piece.  A bin's multiset is
+the sum of its pieces' multisets, so the merged result must be bit-exact
+against the CPU oracle over the whole input -- checked here at sizes the
+oracle finishes quickly, with the pieces made small (FASTKMER_PIECE_BYTES) so
+that inputs of a few MB cross many of them, for key distributions that
+differ from piece to piece.
+"""
+import numpy as np
+import pytest
+
+import fastkmer_amd as fk
+import oracle
+from test_gpu_parity import assert_same_as_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def small_pieces(monkeypatch):
+    monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
+
+
+def count_pinned(fasta, k, m, B=2048, use_ht=False, seq=0, repeat=1):
+    import torch
+    host = torch.empty(max(len(fasta), 1), dtype=torch.uint8).pin_memory()
+    if fasta:
+        host.numpy()[:len(fasta)] = np.frombuffer(fasta, dtype=np.uint8)
+    kc = fk.KmerCounter(k, m, 3, B, use_ht, seq)
+    for _ in range(repeat):
+        kc.ingest_ptr(host.data_ptr(), len(fasta))
+        kc.finish()
+    return kc
+
+
+@pytest.mark.parametrize("k,m,read_len,B", [(28, 10, 100, 2048), (28, 10, 100, 8192), (55, 12, 150, 8192)])
+def test_piece_counts_merge_vs_oracle(small_pieces, k, m, read_len, B):
+    fasta = fk.synth_fasta(40_000 if read_len == 100 else 25_000, read_len, 1_000_000, seed=0xA1 + k)
+    kc = count_pinned(fasta, k, m, B, repeat=2)  # twice: the piece buffers are reused by the second job
+    st = kc.stats()
+    assert st["pieces_counted"] >= 4 and st["fused_map"] == 1
+    ref = oracle.OracleResult(fasta, k, m, B)
+    assert st["kmers"] == ref.total_kmers and st["distinct"] == ref.distinct
+    assert_same_as_oracle(kc, ref)
+
+
+def test_piece_counts_disjoint_and_skewed_pieces(small_pieces):
+    # piece key distributions that share nothing: reads of two unrelated genomes one after the
+    # other, a stretch of one repeated read (a piece holding few keys, with huge counts), and
+    # a low-complexity stretch -- the splitters of a bin come from one piece only, so segments
+    # of the others take several merge rounds
+    a = fk.synth_fasta(12_000, 100, 300_000, seed=0xA2)
+    b = fk.synth_fasta(12_000, 100, 300_000, seed=0xA3, first_read=12_000)
+    rep = b"".join(b">r%010d\n" % i + b"ACGTTGCAAGGCTTACCGATCGGATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAGCATG"
+                   b"CATGCATCGACGTAGCATCG\n" for i in range(6_000))
+    low = b"".join(b">l%d\n" % i + (b"ACACACACAC" * 10) + b"\n" for i in range(6_000))
+    fasta = a + rep + b + low + a[:len(a) // 2]
+    kc = count_pinned(fasta, 28, 10)
+    assert kc.stats()["pieces_counted"] >= 4
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
+
+
+def test_piece_counts_long_sequence(small_pieces):
+    rng = np.random.default_rng(5)
+    seq = np.frombuffer(b"ACGTN", dtype=np.uint8)[rng.choice(5, 3_000_000, p=[.245, .245, .245, .245, .02])]
+    fasta = b">chr synthetic\n" + b"\n".join(seq[i:i + 60].tobytes() for i in range(0, len(seq), 60)) + b"\n"
+    kc = count_pinned(fasta, 28, 10, seq=1)
+    assert kc.stats()["pieces_counted"] >= 4
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048, sequence_type=1))
+
+
+def test_piece_counts_fallback_counts_whole_input(small_pieces):
+    # a 40 KB line after several pieces were counted: the fused map hands the input back, the
+    # piece results are dropped and the whole input is counted by the two-kernel path
+    fasta = fk.synth_fasta(30_000, 100, 600_000, seed=0xA4)
+    cut = len(fasta) * 3 // 4 // 114 * 114
+    fasta = fasta[:cut] + b">" + b"h" * 40_000 + b"\n" + b"ACGT" * 40 + b"\n" + fasta[cut:]
+    kc = count_pinned(fasta, 28, 10)
+    st = kc.stats()
+    assert st["fused_map"] == 0 and st["pieces_counted"] == 0
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
+
+
+def test_piece_counts_hash_mode_counts_once(small_pieces):
+    # useHT=1 (table order does not merge): the whole input is counted in fk_finish
+    fasta = fk.synth_fasta(20_000, 100, 400_000, seed=0xA5)
+    kc = count_pinned(fasta, 28, 10, use_ht=True)
+    assert kc.stats()["pieces_counted"] == 0
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048), ordered=False)
+
+
+def test_piece_counts_many_small_pieces(monkeypatch):
+    # dozens of pieces, each merged into the running result as it is counted
+    monkeypatch.setenv("FASTKMER_INGEST_SEG", str(64 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(64 << 10))
+    fasta = fk.synth_fasta(30_000, 100, 500_000, seed=0xA6)
+    kc = count_pinned(fasta, 28, 10, repeat=2)
+    assert kc.stats()["pieces_counted"] >= 20
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
