@@ -1418,7 +1418,8 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
                          const std::vector<uint64_t> &bin_kmers) {
     hipStream_t s = c->stream;
     const uint32_t nlb = c->nlb, nchunks = (uint32_t)chunks.size();
-    const double per_group = 4096.0 * 0.5;  // LH_TS slots, half full
+    const uint32_t KW = (uint32_t)c->KW;
+    const double per_group = KW == 1 ? 4096.0 * 0.5 : 2048.0 * 0.5;  // LH_TS / LH2_TS slots, half full
     std::vector<uint8_t> flog(nlb, 0);
     std::vector<uint32_t> gbase(nlb + 1, 0);
     std::vector<uint64_t> rec_base(nlb + 1, 0), km_base(nlb + 1, 0);
@@ -1451,8 +1452,8 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     FK_TRY(ensure(c->lh_off, (uint64_t)nchunks * 64 * 8 + 64));
     FK_TRY(ensure(c->lh_groups, (uint64_t)ngroups * sizeof(LhGroup) + 64));
     FK_TRY(ensure(c->lh_recs, nrec * c->W * 8 + 64));
-    FK_TRY(ensure(c->lh_spill[0], nkm * 8 + 64));
-    FK_TRY(ensure(c->lh_okeys, nkm * 8 + 64));
+    FK_TRY(ensure(c->lh_spill[0], nkm * 8 * KW + 64));
+    FK_TRY(ensure(c->lh_okeys, nkm * 8 * KW + 64));
     FK_TRY(ensure(c->lh_ocnt, nkm * 4 + 64));
     FK_TRY(ensure(c->misc, 64));
     FK_TRY(ensure(c->bin_off, ((uint64_t)nlb + 1) * 8));
@@ -1474,9 +1475,11 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     HIP_TRY(hipMemcpyAsync(&spilled, sp_total, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     c->stats.ht_spilled = spilled;
-    // spill rounds: each spilled range is split by a salted key hash into sub-groups of about
-    // per_group keys, so one heavy signature (a group far beyond a table) takes one more round
-    // instead of one per table's worth of keys
+    // spill rounds: each spilled range (a parent) is split by a salted key hash into sub-items of
+    // about per_group keys, so one heavy signature (a group far beyond a table) takes one more
+    // round instead of one per table's worth of keys.  The sub-items of a parent partition its
+    // keys, so they share one spill range of the parent's size (a cursor per parent): a round's
+    // spill space is at most the previous round's spilled keys.
     std::vector<LhItem> prev, items;
     {
         std::vector<uint32_t> cnt(ngroups);
@@ -1487,7 +1490,7 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
             HIP_TRY(hipMemcpy(hg.data(), groups, (uint64_t)ngroups * sizeof(LhGroup), hipMemcpyDeviceToHost));
         }
         for (uint32_t g = 0; spilled && g < ngroups; ++g)
-            if (cnt[g]) prev.push_back(LhItem{hg[g].km_begin, 0, cnt[g], hg[g].lbin, 0, 0});
+            if (cnt[g]) prev.push_back(LhItem{hg[g].km_begin, 0, cnt[g], hg[g].lbin, 0, 0, 0, 0});
     }
     int cur = 0, rounds = 1;
     while (spilled) {
@@ -1495,20 +1498,23 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
         const int nxt = cur ^ 1;
         items.clear();
         uint64_t out = 0;
-        for (const LhItem &p : prev) {
+        std::vector<uint64_t> region(prev.size());
+        for (uint32_t pi = 0; pi < (uint32_t)prev.size(); ++pi) {
+            const LhItem &p = prev[pi];
             int sl = 0;
             while (sl < 16 && (double)(1u << sl) * per_group < (double)p.in_cnt) ++sl;
-            for (uint32_t sub = 0; sub < (1u << sl); ++sub) {
-                items.push_back(LhItem{p.in_base, out, p.in_cnt, p.lbin, sub, (uint32_t)sl});
-                out += p.in_cnt;  // an item spills at most its range's keys
-            }
+            for (uint32_t sub = 0; sub < (1u << sl); ++sub)
+                items.push_back(LhItem{p.in_base, out, p.in_cnt, p.lbin, sub, (uint32_t)sl, pi, 0});
+            region[pi] = out;
+            out += p.in_cnt;  // the parent's sub-items spill at most its keys, together
         }
-        const uint32_t ni = (uint32_t)items.size();
-        FK_TRY(ensure(c->lh_spill[nxt], out * 8 + 64));
+        const uint32_t ni = (uint32_t)items.size(), np = (uint32_t)prev.size();
+        FK_TRY(ensure(c->lh_spill[nxt], out * 8 * KW + 64));
         FK_TRY(ensure(c->lh_items, (uint64_t)ni * sizeof(LhItem) + 64));
         LhItem *d_items = c->lh_items.as<LhItem>();
-        FK_TRY(ensure(c->lh_sp[nxt], (uint64_t)ni * 4 + 64));
+        FK_TRY(ensure(c->lh_sp[nxt], (uint64_t)np * 4 + 64));
         HIP_TRY(hipMemcpyAsync(d_items, items.data(), (uint64_t)ni * sizeof(LhItem), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(c->lh_sp[nxt].p, 0, (uint64_t)np * 4, s));
         HIP_TRY(hipMemsetAsync(sp_total, 0, 8, s));
         HIP_TRY(launch_ht_combine(c->W, c->lh_spill[cur].as<uint64_t>(), groups, d_items, ni, c->cfg.k,
                                   (uint32_t)rounds, c->lh_spill[nxt].as<uint64_t>(), c->lh_sp[nxt].as<uint32_t>(),
@@ -1516,13 +1522,15 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
                                   c->lh_ocnt.as<uint32_t>(), s));
         HIP_TRY(hipMemcpyAsync(&spilled, sp_total, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        prev.clear();
+        c->stats.ht_spilled += spilled;
+        std::vector<LhItem> next;
         if (spilled) {
-            std::vector<uint32_t> cnt(ni);
-            HIP_TRY(hipMemcpy(cnt.data(), c->lh_sp[nxt].p, (uint64_t)ni * 4, hipMemcpyDeviceToHost));
-            for (uint32_t i = 0; i < ni; ++i)
-                if (cnt[i]) prev.push_back(LhItem{items[i].out_base, 0, cnt[i], items[i].lbin, 0, 0});
+            std::vector<uint32_t> cnt(np);
+            HIP_TRY(hipMemcpy(cnt.data(), c->lh_sp[nxt].p, (uint64_t)np * 4, hipMemcpyDeviceToHost));
+            for (uint32_t pi = 0; pi < np; ++pi)
+                if (cnt[pi]) next.push_back(LhItem{region[pi], 0, cnt[pi], prev[pi].lbin, 0, 0, 0, 0});
         }
+        prev.swap(next);
         cur = nxt;
     }
     c->stats.ht_rounds = (uint64_t)rounds;
@@ -1532,9 +1540,9 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     uint64_t distinct = 0;
     HIP_TRY(hipMemcpyAsync(&distinct, c->bin_off.as<uint64_t>() + nlb, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    FK_TRY(ensure(c->dense_keys, distinct * 8 + 64));
+    FK_TRY(ensure(c->dense_keys, distinct * 8 * KW + 64));
     FK_TRY(ensure(c->dense_counts, distinct * 4 + 64));
-    HIP_TRY(launch_ht_gather(d_km_base, c->bin_off.as<uint64_t>(), nlb, c->lh_okeys.as<uint64_t>(),
+    HIP_TRY(launch_ht_gather((int)KW, d_km_base, c->bin_off.as<uint64_t>(), nlb, c->lh_okeys.as<uint64_t>(),
                              c->lh_ocnt.as<uint32_t>(), c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(),
                              s));
     c->distinct = distinct;
@@ -1621,7 +1629,7 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
         max_bin = std::max(max_bin, bkm[lb]);
     }
     HIP_TRY(hipEventRecord(c->ev[6], s));
-    if (c->cfg.use_ht && c->lh_mode && c->KW == 1)
+    if (c->cfg.use_ht && c->lh_mode && c->cfg.k <= 63)  // k = 64: no spare bit in the hi word (global tables)
         FK_TRY(reduce_ht_lds(c, chunks, bcb, bkm));
     else if (c->cfg.use_ht)
         FK_TRY(reduce_ht(c, nchunks, bkm));

@@ -201,7 +201,7 @@ hipError_t launch_ht_compact(int KW, const uint64_t *tkeys, const uint32_t *tcou
 hipError_t launch_ht_bin_offsets(const uint64_t *slot_scan, const uint64_t *table_off, uint32_t nlbins,
                                  uint64_t total, uint64_t *bin_off, hipStream_t s);
 
-// ---- hash count in LDS tables (fk_count_lds.inc), k <= 32
+// ---- hash count in LDS tables (fk_count_lds.inc), k <= 63 (64-bit keys up to k = 32, 128-bit above)
 struct LhGroup {          // one (local bin, fine value) group of records
     uint64_t rec_begin;   // first record in the fine-partitioned array
     uint64_t km_begin;    // first k-mer slot (prefix of the groups' k-mers): round-1 spill range
@@ -213,18 +213,21 @@ hipError_t launch_fine_partition(int W, const uint64_t *rec, const Chunk *chunks
                                  const uint32_t *bcb, uint32_t nlb, const uint8_t *flog, const uint64_t *rec_base,
                                  const uint64_t *km_base, const uint32_t *gbase, uint32_t *Hr, uint32_t *Hk,
                                  uint64_t *off, LhGroup *groups, uint64_t *out, hipStream_t s);
-struct LhItem {            // one work item of a spill round: the spilled keys of a group (or of an
-    uint64_t in_base;     // item of the previous round) whose salted key hash selects `sub`
-    uint64_t out_base;    // spill range of this item (in_cnt slots)
+struct LhItem {            // one work item of a spill round: the keys of a parent range (the spill of a
+    uint64_t in_base;     // group, or of a parent of the previous round) whose salted key hash selects `sub`
+    uint64_t out_base;    // the parent's spill range (in_cnt slots, shared by its 2^slog sub-items)
     uint32_t in_cnt, lbin, sub, slog;
+    uint32_t parent, pad; // spill cursor of the parent (sp_cnt[parent])
 };
-// items == null: round 1 over groups[0..n); else spill round over items[0..n)
+// items == null: round 1 over groups[0..n), sp_cnt[g] = keys group g spilled; else a spill round
+// over items[0..n), sp_cnt[parent] = the spill cursor of each parent (zeroed by the caller)
 hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, const LhItem *items, uint32_t n,
                              int k, uint32_t salt, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
                              const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys, uint32_t *ocnt,
                              hipStream_t s, int probe = 0);
-hipError_t launch_ht_gather(const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb, const uint64_t *okeys,
-                            const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt, hipStream_t s);
+hipError_t launch_ht_gather(int KW, const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb,
+                            const uint64_t *okeys, const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt,
+                            hipStream_t s);
 
 // ---- merge of two count results (fk_merge.inc): the per-bin union, equal k-mers' counts added
 struct MergeSrc {          // one result

@@ -271,6 +271,9 @@ def execute_job_distributed(configuration, group=None, device=None, rounds=None)
     return kc
 
 
+SIG_DENSE_MAX = (1 << 24) + 1  # m <= 12: the dense signature counts are all-reduced whole
+
+
 def execute_find_bin_signatures_job_distributed(configuration, group=None, device=None):
     """executeFindBinSignaturesJob (SBKC:956-986) for one rank of a job.
 
@@ -281,7 +284,10 @@ def execute_find_bin_signatures_job_distributed(configuration, group=None, devic
     (sharding.read_record_shard), so the merged counts are the whole file's; a
     long sequence (sequenceType 1) is cut between ranks with the k - 1 overlap
     (sharding.read_shard), and a super-k-mer over a cut counts once per side, as
-    over the reference's input splits.  Returns the merged counts (device tensor)."""
+    over the reference's input splits: the merged counts then depend on the number
+    of ranks (they equal the sum of every rank's own signature counts of its piece,
+    tests/test_distributed.py pins that), as the reference's depend on its HDFS
+    splits.  Returns the merged counts (device tensor)."""
     import fastkmer_amd as fk
     from fastkmer_amd.sharding import read_record_shard, read_shard
 
@@ -296,7 +302,17 @@ def execute_find_bin_signatures_job_distributed(configuration, group=None, devic
                         device=dev.index if dev.index is not None else -1) as kc:
         kc.ingest(piece)
         counts = kc.signature_counts()
-        if dist.get_backend(group) == "gloo":
+        if counts.numel() > SIG_DENSE_MAX:
+            # large m (4^m + 1 slots up to 8.6 GB at m = 15): only the signatures that occur travel,
+            # as the reference's reduceByKey only ever holds those
+            idx = torch.nonzero(counts).flatten()
+            mine = (idx.cpu(), counts[idx].cpu())
+            parts = [None] * world
+            dist.all_gather_object(parts, mine, group=group)
+            counts.zero_()
+            for i, v in parts:
+                counts.index_add_(0, i.to(counts.device), v.to(counts.device))
+        elif dist.get_backend(group) == "gloo":
             host = counts.cpu()
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
             counts.copy_(host)

@@ -74,7 +74,7 @@ typedef struct fk_stats {
     double ms_h2d;             /* last fk_ingest: host-to-device copy, first segment issued to last landed */
     uint64_t fused_fallback;   /* why the fused kernel handed the input back: 1 long line, 2 text before the
                                   first header, 4 halo too short, 8 too many records in a tile (0: none) */
-    uint64_t ht_spilled;       /* useHT LDS tables: keys the first round spilled (counted by later rounds) */
+    uint64_t ht_spilled;       /* useHT LDS tables: keys spilled over all rounds (each counted by a later round) */
     uint64_t ht_rounds;        /* useHT LDS tables: rounds until every key was counted */
     /* multi-rank exchange inside the context (fk_comm_init*), last fk_finish */
     uint64_t xch_steps;        /* exchange steps (pieces sent during fk_ingest, the last piece, closing steps) */

@@ -271,6 +271,31 @@ def test_find_bin_signatures_job_distributed(tmp_path, world):
     assert len(want) > 100 and got == want
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_find_bin_signatures_job_distributed_long_sequence(tmp_path, world):
+    """sequenceType = 1 with m = 13: one record cut into byte ranges with the k - 1 overlap
+    (read_shard, as the reference's input splits cut it); a super-k-mer across a cut counts once
+    per side, so the merged files equal the sum of every rank's own getBinSignatures over its
+    piece -- the semantics this job pins -- and they differ from a one-rank run.  4^13 + 1 slots
+    exceed the dense all-reduce: only the signatures that occur travel (all_gather of pairs)."""
+    from fastkmer_amd.sharding import read_shard
+    k, m, B = 28, 13, 4096
+    data = _long_fasta()
+    path = tmp_path / "long.fa"
+    path.write_bytes(data)
+    cfg = dict(dataset=str(path), outputDirectory=str(tmp_path / "out") + "/", k=k, m=m, x=3, max_b=B,
+               sequenceType=1)
+    mp.spawn(_binsig_worker, args=(world, _free_port(), cfg), nprocs=world, join=True)
+    got = _read_bins(fk.TestConfiguration(**cfg).outputDir)
+    want_counts = sum(oracle.bin_signatures(read_shard(str(path), world, r, k).piece, k, m) for r in range(world))
+    ref_dir = tmp_path / "ref"
+    oracle.write_bin_signatures(want_counts, m, B, str(ref_dir))
+    assert got == _read_bins(str(ref_dir)) and len(got) > 10
+    one = oracle.bin_signatures(data, k, m)
+    assert int(want_counts.sum()) >= int(one.sum())  # the cuts add super-k-mers, never remove any
+
+
 # ---------------------------------------------------------------- per-rank file reads (CPU)
 
 def _fasta_variants():
