@@ -3,7 +3,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out/prof_pieces
-FASTKMER_PIECE_BYTES=268435456 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pieces -o run --output-format csv -- python -u scripts/pieces_probe.py 256 > gpurun_out/prof_pieces.log 2>&1 || { tail -20 gpurun_out/prof_pieces.log; exit 1; }
+FASTKMER_PIECE_BYTES=536870912 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pieces -o run --output-format csv -- python -u scripts/pieces_probe.py 512 > gpurun_out/prof_pieces.log 2>&1 || { tail -20 gpurun_out/prof_pieces.log; exit 1; }
 find gpurun_out/prof_pieces -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/pieces_kernel_stats.csv
 python - <<'PY'
 import csv

@@ -177,6 +177,9 @@ def test_c4_per_gpu_load_rank0_properties():
     with fk.KmerCounter(k, m, X, b, False, 0, n_ranks=G, rank=0) as kc:
         kc.reduce(recv.data_ptr(), total_rec)
         torch.cuda.synchronize()
+        cold = kc.stats()
+        kc.reduce(recv.data_ptr(), total_rec)  # again with the context's buffers allocated (steady state)
+        torch.cuda.synchronize()
         del recv
         torch.cuda.empty_cache()
         st = kc.stats()
@@ -199,7 +202,8 @@ def test_c4_per_gpu_load_rank0_properties():
                           for j in range(k - m + 1))
                 assert oracle.hash_to_bucket(sig, b) == bb
         print(f"configs[3] rank 0: {total_rec} records, {int(sent_kmers[own].sum())} k-mers, {st['distinct']} "
-              f"distinct, count stage {st['ms_count']:.1f} ms, partition {st['ms_partition']:.1f} ms")
+              f"distinct, count stage {st['ms_count']:.1f} ms (first call, buffers allocated inside: "
+              f"{cold['ms_count']:.1f} ms), partition {st['ms_partition']:.1f} ms, F={st['fine_bits']}")
 
 
 def _c5_job(path, world=8):
