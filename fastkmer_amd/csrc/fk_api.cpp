@@ -55,6 +55,33 @@ int set_err(int code, const char *fmt, ...) {
         if (r_ != FK_OK) return r_; \
     } while (0)
 
+// Grow-only pinned host memory: small uploads and read-backs on the hot path go
+// through it (pageable transfers are staged by the runtime, and block the host).
+struct PinBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need) {
+        if (bytes >= need) return FK_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        const size_t want = std::max<size_t>(need + need / 4, 4096);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return FK_E_NOMEM;
+        }
+        bytes = want;
+        return FK_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
@@ -289,6 +316,7 @@ struct fk_ctx {
     double ms_h2d = 0.0;  // last fk_ingest: first copy issued -> last copy done
     bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
+    PinBuf pin_up, pin_down, pin_merge;  // staging: chunk tables up, per-bin counts down, merge tables up
 
     // multi-rank exchange inside the context (fk_comm_init / fk_comm_init_local): the input
     // is emitted in pieces grouped by (destination, local bin) and each piece is exchanged
@@ -308,7 +336,7 @@ struct fk_ctx {
     uint64_t tiles_counted = 0;   // one rank: tiled records [0, tiles_counted) counted
     size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) counted
     double acc_ms_part = 0.0, acc_ms_count = 0.0, acc_ms_merge = 0.0;  // the job's earlier pieces
-    DevBuf m2_tile_bin, m2_bin_tile0, m2_split_a, m2_split_b, m2_bnd, m2_tcount, m2_toff, m2_keys, m2_counts;
+    DevBuf m2_bin_tile0, m2_split_a, m2_split_b, m2_bnd, m2_tcount, m2_toff, m2_keys, m2_counts;
 
     fk::Comm *comm = nullptr;
     hipStream_t comm_stream = nullptr;
@@ -552,11 +580,14 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     delete c->comm;
     c->comm = nullptr;
+    c->pin_up.release();
+    c->pin_down.release();
+    c->pin_merge.release();
     release(c->xsend);
     release(c->xrecv);
     for (fk_ctx::PieceRes *r : {&c->acc, &c->acc2, &c->tmp})
         for (DevBuf *b : {&r->keys, &r->counts, &r->bin_off}) release(*b);
-    for (DevBuf *b : {&c->m2_tile_bin, &c->m2_bin_tile0, &c->m2_split_a, &c->m2_split_b, &c->m2_bnd, &c->m2_tcount,
+    for (DevBuf *b : {&c->m2_bin_tile0, &c->m2_split_a, &c->m2_split_b, &c->m2_bnd, &c->m2_tcount,
                       &c->m2_toff, &c->m2_keys, &c->m2_counts})
         release(*b);
     for (auto &e : c->xev)
@@ -1637,8 +1668,10 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
         FK_TRY(reduce_sorted(c, nchunks, total_kmers, max_bin));
     HIP_TRY(hipEventRecord(c->ev[7], s));
     c->h_bin_off.assign((size_t)nlb + 1, 0);
-    HIP_TRY(hipMemcpyAsync(c->h_bin_off.data(), c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    memcpy(c->h_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
     c->stats.records_received = nrecv;
     c->stats.distinct = c->distinct;
     c->stats.ms_partition = ev_ms(c->ev[4], c->ev[5]);
@@ -1653,8 +1686,13 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     const uint32_t nchunks = (uint32_t)chunks.size();
     FK_TRY(ensure(c->chunks, nchunks * sizeof(Chunk)));
     FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)c->nlb + 1) * 4));
-    if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, chunks.data(), nchunks * sizeof(Chunk), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, bcb.data(), ((uint64_t)c->nlb + 1) * 4, hipMemcpyHostToDevice, s));
+    // the previous upload through the staging buffer is complete: the count that used it synchronized
+    const size_t cb = (size_t)nchunks * sizeof(Chunk), bb = ((size_t)c->nlb + 1) * 4;
+    if (c->pin_up.ensure(cb + bb)) return set_err(FK_E_NOMEM, "hipHostMalloc(%zu) failed", cb + bb);
+    memcpy(c->pin_up.p, chunks.data(), cb);
+    memcpy(c->pin_up.as<uint8_t>() + cb, bcb.data(), bb);
+    if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, c->pin_up.p, cb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, c->pin_up.as<uint8_t>() + cb, bb, hipMemcpyHostToDevice, s));
     c->h_bcb = bcb;
     return FK_OK;
 }
@@ -1669,11 +1707,16 @@ static int reduce_src(fk_ctx *c, const RecSrc &src) {
     HIP_TRY(hipEventRecord(c->ev[4], s));
     FK_TRY(part_count(c->part, src, 1, c->G, local_table(c), nlb, c->ws, s));
     std::vector<uint64_t> brec(nlb), bkm(nlb);
+    if (c->pin_down.ensure((size_t)nlb * 16 + 16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
     if (nlb) {
-        HIP_TRY(hipMemcpyAsync(brec.data(), c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(bkm.data(), c->part.kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->pin_down.as<uint64_t>() + nlb, c->part.kmer.p, nlb * 8, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
+    if (nlb) {
+        memcpy(brec.data(), c->pin_down.p, nlb * 8);
+        memcpy(bkm.data(), c->pin_down.as<uint64_t>() + nlb, nlb * 8);
+    }
     // record offsets per local bin after the partition
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
     uint64_t off = 0;
@@ -1823,15 +1866,16 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
     hipStream_t s = c->stream;
     const uint32_t nlb = c->nlb;
     const double t0 = now_ms();
-    std::vector<uint32_t> tile_bin, bin_tile0(nlb);
-    tile_bin.reserve((a.distinct + b.distinct) / MERGE_TILE + nlb + 1);
+    // every bin's first tile (bins have ceil(n / MERGE_TILE) >= 1 tiles), staged in pinned memory
+    if (c->pin_merge.ensure(((size_t)nlb + 1) * 4)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    uint32_t *bin_tile0 = c->pin_merge.as<uint32_t>();
+    uint64_t ntiles = 0;
     for (uint32_t lb = 0; lb < nlb; ++lb) {
         const uint64_t n = a.h_bin_off[lb + 1] - a.h_bin_off[lb] + b.h_bin_off[lb + 1] - b.h_bin_off[lb];
-        const uint64_t nt = std::max<uint64_t>(1, (n + MERGE_TILE - 1) / MERGE_TILE);
-        bin_tile0[lb] = (uint32_t)tile_bin.size();
-        tile_bin.insert(tile_bin.end(), nt, lb);
+        bin_tile0[lb] = (uint32_t)ntiles;
+        ntiles += std::max<uint64_t>(1, (n + MERGE_TILE - 1) / MERGE_TILE);
     }
-    const uint64_t ntiles = tile_bin.size();
+    bin_tile0[nlb] = (uint32_t)ntiles;
     if (!ntiles) {  // no local bins
         oh_bin_off.assign(1, 0);
         *odistinct = 0;
@@ -1840,8 +1884,7 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
         return FK_OK;
     }
     HIP_TRY(hipEventRecord(c->ev[6], s));
-    FK_TRY(ensure(c->m2_tile_bin, ntiles * 4));
-    FK_TRY(ensure(c->m2_bin_tile0, (uint64_t)nlb * 4));
+    FK_TRY(ensure(c->m2_bin_tile0, ((uint64_t)nlb + 1) * 4));
     FK_TRY(ensure(c->m2_split_a, (ntiles + 1) * 8));
     FK_TRY(ensure(c->m2_split_b, (ntiles + 1) * 8));
     FK_TRY(ensure(c->m2_bnd, (ntiles + 1) * 8));
@@ -1849,10 +1892,9 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
     FK_TRY(ensure(c->m2_toff, (ntiles + 1) * 8));
     FK_TRY(ensure(c->m2_keys, ntiles * MERGE_TILE * 8 * c->KW));
     FK_TRY(ensure(c->m2_counts, ntiles * MERGE_TILE * 4));
-    HIP_TRY(hipMemcpyAsync(c->m2_tile_bin.p, tile_bin.data(), ntiles * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->m2_bin_tile0.p, bin_tile0.data(), (uint64_t)nlb * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->m2_bin_tile0.p, bin_tile0, ((uint64_t)nlb + 1) * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(launch_merge2(c->KW, merge_src(a.keys, a.counts, a.bin_off), merge_src(b.keys, b.counts, b.bin_off),
-                          c->m2_tile_bin.as<uint32_t>(), c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles,
+                          c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles,
                           c->m2_split_a.as<uint64_t>(), c->m2_split_b.as<uint64_t>(), c->m2_bnd.as<uint64_t>(),
                           c->m2_tcount.as<uint32_t>(), c->m2_keys.as<uint64_t>(), c->m2_counts.as<uint32_t>(), s));
     HIP_TRY(scan_excl_sum_u32_to_u64(c->m2_tcount.as<uint32_t>(), c->m2_toff.as<uint64_t>(), ntiles,
@@ -1869,8 +1911,10 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
                                obin_off.as<uint64_t>(), s));
     HIP_TRY(hipEventRecord(c->ev[7], s));
     oh_bin_off.assign((size_t)nlb + 1, 0);
-    HIP_TRY(hipMemcpyAsync(oh_bin_off.data(), obin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    HIP_TRY(hipMemcpyAsync(c->pin_down.p, obin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    memcpy(oh_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
     *odistinct = oh_bin_off[nlb];
     c->acc_ms_merge += ev_ms(c->ev[6], c->ev[7]);
     c->stats.ms_total += now_ms() - t0;

@@ -236,13 +236,12 @@ struct MergeSrc {          // one result
     const uint64_t *bin_off;  // [nlb + 1]
 };
 constexpr uint32_t MERGE_TILE = 1024;  // merged entries per workgroup (M2_TILE)
-// tile_bin[ntiles]: the bin of every tile (each bin has ceil((na + nb) / MERGE_TILE) >= 1 tiles, in
-// bin order), bin_tile0[nlb]: its first tile; split_a / split_b / bnd: ntiles + 1 u64; tcount: ntiles;
+// bin_tile0[nlb + 1]: every bin's first tile (a bin has ceil((na + nb) / MERGE_TILE) >= 1 tiles, in
+// bin order; bin_tile0[nlb] = ntiles); split_a / split_b / bnd: ntiles + 1 u64; tcount: ntiles;
 // sparse keys / counts: ntiles * MERGE_TILE entries (every tile's slot)
-hipError_t launch_merge2(int KW, const MergeSrc &A, const MergeSrc &B, const uint32_t *tile_bin,
-                         const uint32_t *bin_tile0, uint32_t nlb, uint64_t ntiles, uint64_t *split_a, uint64_t *split_b,
-                         uint64_t *bnd, uint32_t *tcount, uint64_t *sparse_keys, uint32_t *sparse_counts,
-                         hipStream_t s);
+hipError_t launch_merge2(int KW, const MergeSrc &A, const MergeSrc &B, const uint32_t *bin_tile0, uint32_t nlb,
+                         uint64_t ntiles, uint64_t *split_a, uint64_t *split_b, uint64_t *bnd, uint32_t *tcount,
+                         uint64_t *sparse_keys, uint32_t *sparse_counts, hipStream_t s);
 // toff = exclusive scan of tcount (ntiles + 1): the dense result and its bin offsets (nlb + 1)
 hipError_t launch_merge2_pack(int KW, const uint32_t *tcount, const uint64_t *toff, const uint32_t *bin_tile0,
                               uint32_t nlb, uint64_t ntiles, const uint64_t *sparse_keys, const uint32_t *sparse_counts,

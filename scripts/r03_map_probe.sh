@@ -1,5 +1,5 @@
 #!/bin/bash
 # Fused map phases: full kernel, stop after byte classes + line state (probe 1), after compaction (probe 2)
-for p in 0 1 2; do
+for p in 0 1 2 3 4; do
   FASTKMER_FUSED_PROBE=$p FK_MAP_REPS=9 timeout -k 10 120 python -u scripts/map_once.py | sed "s/^/probe $p: /" || exit 1
 done
