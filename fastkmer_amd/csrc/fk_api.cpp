@@ -284,6 +284,8 @@ struct fk_ctx {
     DevBuf records, counters, sig_status, sig_kmers;
     DevBuf tcnt;                  // fused map: records per tile (tiled record layout)
     DevBuf rec_hdr;               // fused map: every record's header word, in the record's tile slot
+    DevBuf rec_pos;               // fused map: every record's first position in its tile's code stream (u16)
+    DevBuf rec_code;              // fused map: per tile, the tile's 2-bit code stream (map_fused_cslot() words)
     DevBuf tstat;                 // fused map: per tile (k-mers, positions)
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
@@ -563,7 +565,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
-                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->tstat,
+                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
                       &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
@@ -669,15 +671,15 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
     const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
     if (end <= c->pm_tiles) return FK_OK;
-    if (c->tcnt.bytes < end * 4 || c->tstat.bytes < end * 8 || c->records.bytes < end * map_fused_tcap() * c->W * 8 ||
-        c->rec_hdr.bytes < end * map_fused_tcap() * 4)
+    if (c->tcnt.bytes < end * 4 || c->tstat.bytes < end * 8 || c->rec_hdr.bytes < end * map_fused_tcap() * 4 ||
+        c->rec_pos.bytes < end * map_fused_tcap() * 2 || c->rec_code.bytes < end * map_fused_cslot() * 4)
         return set_err(FK_E_STATE, "streamed map: %llu tiles exceed the reserved record slots",
                        (unsigned long long)end);
     hipStream_t s = c->stream;
     if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
-                             end - c->pm_tiles, c->fm, c->records.as<uint64_t>(), c->rec_hdr.as<uint32_t>(),
-                             c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(),
+                             end - c->pm_tiles, c->fm, c->rec_hdr.as<uint32_t>(), c->rec_pos.as<uint16_t>(),
+                             c->rec_code.as<uint32_t>(), c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(),
                              c->counters.as<unsigned long long>(), s, c->fused_probe));
     c->pm_tiles = end;
     if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
@@ -735,10 +737,11 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         const uint64_t tiles = (need + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
         if (c->tcnt.bytes < tiles * 4) FK_TRY(grow_keep(c->tcnt, tiles * 4, c->tcnt.bytes, s));
         if (c->tstat.bytes < tiles * 8) FK_TRY(grow_keep(c->tstat, tiles * 8, c->tstat.bytes, s));
-        const uint64_t rec_need = tiles * map_fused_tcap() * c->W * 8;
-        if (c->records.bytes < rec_need) FK_TRY(grow_keep(c->records, rec_need, c->records.bytes, s));
-        const uint64_t hdr_need = tiles * map_fused_tcap() * 4;
+        const uint64_t hdr_need = tiles * map_fused_tcap() * 4, pos_need = tiles * map_fused_tcap() * 2;
+        const uint64_t code_need = tiles * map_fused_cslot() * 4;
         if (c->rec_hdr.bytes < hdr_need) FK_TRY(grow_keep(c->rec_hdr, hdr_need, c->rec_hdr.bytes, s));
+        if (c->rec_pos.bytes < pos_need) FK_TRY(grow_keep(c->rec_pos, pos_need, c->rec_pos.bytes, s));
+        if (c->rec_code.bytes < code_need) FK_TRY(grow_keep(c->rec_code, code_need, c->rec_code.bytes, s));
         if (fresh) {
             FK_TRY(ensure(c->counters, 64));
             HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
@@ -821,8 +824,9 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
     FK_TRY(ensure(c->fasta_own, total_bytes));
     if (premap_eligible(c)) {
         const uint64_t tiles = (total_bytes + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
-        FK_TRY(ensure(c->records, tiles * map_fused_tcap() * c->W * 8));
         FK_TRY(ensure(c->rec_hdr, tiles * map_fused_tcap() * 4));
+        FK_TRY(ensure(c->rec_pos, tiles * map_fused_tcap() * 2));
+        FK_TRY(ensure(c->rec_code, tiles * map_fused_cslot() * 4));
         FK_TRY(ensure(c->tcnt, tiles * 4));
         FK_TRY(ensure(c->tstat, tiles * 8));
     }
@@ -903,14 +907,16 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     FK_TRY(ensure(c->tcnt, ntiles * 4));
     FK_TRY(ensure(c->tstat, ntiles * 8));
     FK_TRY(ensure(c->counters, 64));
-    FK_TRY(ensure(c->records, ntiles * map_fused_tcap() * c->W * 8));
     FK_TRY(ensure(c->rec_hdr, ntiles * map_fused_tcap() * 4));
+    FK_TRY(ensure(c->rec_pos, ntiles * map_fused_tcap() * 2));
+    FK_TRY(ensure(c->rec_code, ntiles * map_fused_cslot() * 4));
     HIP_TRY(hipEventRecord(c->ev[2], s));
     HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
     HIP_TRY(hipEventRecord(c->ev[10], s));
     HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, c->fm,
-                             c->records.as<uint64_t>(), c->rec_hdr.as<uint32_t>(), c->tcnt.as<uint32_t>(),
-                             c->tstat.as<uint32_t>(), c->counters.as<unsigned long long>(), s, c->fused_probe));
+                             c->rec_hdr.as<uint32_t>(), c->rec_pos.as<uint16_t>(), c->rec_code.as<uint32_t>(),
+                             c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), c->counters.as<unsigned long long>(), s,
+                             c->fused_probe));
     HIP_TRY(hipEventRecord(c->ev[11], s));
     HIP_TRY(launch_tile_totals(c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), ntiles,
                                c->counters.as<unsigned long long>(), s));
@@ -933,11 +939,17 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     return FK_OK;
 }
 
+// the fused map's tiles [t0, t0 + nt) as a partition source (nrec: their records, or a bound)
+static RecSrc fused_src(const fk_ctx *c, uint64_t t0, uint64_t nt, uint64_t nrec) {
+    const uint64_t tcap = map_fused_tcap(), cslot = map_fused_cslot();
+    return tiled_src(c->rec_hdr.as<uint32_t>() + t0 * tcap, c->rec_pos.as<uint16_t>() + t0 * tcap,
+                     c->rec_code.as<uint32_t>() + t0 * cslot, c->tcnt.as<uint32_t>() + t0, nrec, nt, (uint32_t)tcap,
+                     (uint32_t)cslot, c->W, c->cfg.k);
+}
+
 // the records of the last fk_map as a partition source
 static RecSrc map_src(const fk_ctx *c) {
-    if (c->rec_tiled)
-        return tiled_src(c->records.as<uint64_t>(), c->tcnt.as<uint32_t>(), c->nrec, c->rec_tiles, map_fused_tcap(),
-                         c->W, c->rec_hdr.as<uint32_t>());
+    if (c->rec_tiled) return fused_src(c, 0, c->rec_tiles, c->nrec);
     return dense_src(c->records.as<uint64_t>(), c->nrec, c->W);
 }
 
@@ -1972,9 +1984,7 @@ static int local_maybe_piece(fk_ctx *c) {
         return FK_OK;
     }
     const uint64_t t0 = c->tiles_counted, nt = c->pm_tiles - t0;
-    const uint32_t tcap = map_fused_tcap();
-    const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
-                                 nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
+    const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
     c->tiles_counted = c->pm_tiles;
     return count_piece(c, [&] { return reduce_src(c, src); }, false);
 }
@@ -2199,9 +2209,7 @@ static int xch_maybe_piece(fk_ctx *c) {
         return FK_OK;
     }
     const uint64_t t0 = c->xch.tiles_sent, nt = c->pm_tiles - t0;
-    const uint32_t tcap = map_fused_tcap();
-    const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
-                                 nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
+    const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
     c->xch.tiles_sent = c->pm_tiles;
     const size_t before = c->xch.segs.size();
     const int rc = xch_step(c, &src, 0);
@@ -2223,9 +2231,7 @@ static int finish_exchange(fk_ctx *c) {
     uint64_t flags = XF_FINAL;
     if (c->rec_tiled && pieced && !c->xch.stop_pieces && tiles_sent <= c->rec_tiles) {
         const uint64_t nt = c->rec_tiles - tiles_sent;
-        const uint32_t tcap = map_fused_tcap();
-        src = tiled_src(c->records.as<uint64_t>() + tiles_sent * tcap * c->W, c->tcnt.as<uint32_t>() + tiles_sent,
-                        nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + tiles_sent * tcap);
+        src = fused_src(c, tiles_sent, nt, nt * map_fused_tcap());
     } else {
         src = map_src(c);
         if (pieced) flags |= XF_RETRACT;
@@ -2281,9 +2287,7 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
         const bool more = c->rec_tiles > c->tiles_counted;
         if (more) {
             const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
-            const uint32_t tcap = map_fused_tcap();
-            const RecSrc src = tiled_src(c->records.as<uint64_t>() + t0 * tcap * c->W, c->tcnt.as<uint32_t>() + t0,
-                                         nt * tcap, nt, tcap, c->W, c->rec_hdr.as<uint32_t>() + t0 * tcap);
+            const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
             FK_TRY(count_piece(c, [&] { return reduce_src(c, src); }, true));
         }
         finish_pieces(c, more);

@@ -5,6 +5,8 @@
 //   codes      u32[npos/16 + pad]        2-bit bases, 16 per word, MSB-first
 //   valid      u32[npos/32 + pad]        1 bit per position (1 = A/C/G/T)
 //   records    u64[W * nrec]             super-k-mer records, W = 2 (k<=32) or 3
+//              (the fused map: per tile, a header word + a u16 position per record and the
+//              tile's 2-bit code stream; the partition builds the W-word records from them)
 //   keys       u64[KW * nkmers]          canonical k-mers scattered by (bin, cell)
 //   out_keys   u64[KW * nkmers]          per-bucket sorted unique keys
 //   dense      u64[KW * distinct] + u32 counts, bin_off[nbins_local + 1]
@@ -69,42 +71,53 @@ hipError_t launch_bin_signatures(const uint32_t *codes, const uint32_t *valid, u
 hipError_t launch_sig_compact(const unsigned long long *counts, uint64_t n, uint64_t *pairs, unsigned long long *nout,
                               hipStream_t s);
 
-// ---- fused parse + signature (fk_map_fused.inc): FASTA bytes -> records in one kernel
+// ---- fused parse + signature (fk_map_fused.inc): FASTA bytes -> compact records in one kernel
 // for (k, m) with an instantiation; tiles of fm_tile_bytes(nth) FASTA bytes (nth = 256 or 512
-// threads).  Tile t's records go to records + t * map_fused_tcap() * W words, their count to
-// tcnt[t]; counters[4] (zeroed) = records, k-mers, fallback flags, positions.
+// threads).  Tile t's records are header words at hdrs + t * map_fused_tcap() and their first
+// positions at pos + t * map_fused_tcap(), their count in tcnt[t]; the tile's 2-bit code stream
+// (MSB-first, 16 bases per word) at codes + t * map_fused_cslot().  counters[4] (zeroed) =
+// records, k-mers, fallback flags, positions.
 bool map_fused_supported(int k, int m, uint32_t nbins);
 uint64_t fm_tile_bytes(int nth);
 uint64_t fm_span_bytes(int nth);
 uint32_t map_fused_tcap();
+uint32_t map_fused_cslot();
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
-                            uint64_t ntiles, FastMod fm, uint64_t *records, uint32_t *hdrs, uint32_t *tcnt,
-                            uint32_t *tstat, unsigned long long *counters, hipStream_t s, int probe = 0);
+                            uint64_t ntiles, FastMod fm, uint32_t *hdrs, uint16_t *pos, uint32_t *codes,
+                            uint32_t *tcnt, uint32_t *tstat, unsigned long long *counters, hipStream_t s,
+                            int probe = 0);
 // counters[0] / [1] / [3] = records / k-mers / positions summed over the fused map's tiles [0, ntiles)
 hipError_t launch_tile_totals(const uint32_t *tcnt, const uint32_t *tstat, uint64_t ntiles,
                               unsigned long long *counters, hipStream_t s);
 
-// ---- records to partition: dense (tcnt == null: nrec records, cut into PART_TILE tiles) or
-// tiled, as the fused map writes them (tile t holds tcnt[t] records at rec + t * tcap * W).
+// ---- records to partition: dense (tcnt == null: nrec W-word records, cut into PART_TILE tiles)
+// or the fused map's compact tiles (tile t holds tcnt[t] records: slot t * tcap + j has the
+// header word hdr[.] and the first position pos[.] of its bases in the tile's code stream
+// code + t * cslot; the partition builds the W-word record from them).
 constexpr uint32_t PART_TILE = 4096;  // dense records per tile
 constexpr uint32_t PART_TPC = 4;      // tiles per partition workgroup (dense: 16384 records)
 constexpr uint32_t PART_SEG = 64;     // partition workgroups per segment of the histogram scan
 inline uint32_t part_segments(uint32_t nwg) { return (nwg + PART_SEG - 1) / PART_SEG; }
 struct RecSrc {
-    const uint64_t *rec;
+    const uint64_t *rec;   // dense records (null for compact tiles)
     const uint32_t *tcnt;  // null: dense
     uint64_t nrec;         // records (the sum of tcnt when tiled)
     uint64_t ntiles;
     uint32_t tcap;         // record slots per tile
     uint32_t W;            // u64 words per record
-    const uint32_t *hdr;   // tiled: the records' header words in the same slots (null: read the records)
+    const uint32_t *hdr;   // compact tiles: header word per record slot
+    const uint16_t *pos;   // compact tiles: first position of the record's bases in its tile's stream
+    const uint32_t *code;  // compact tiles: per tile, cslot words of 2-bit codes (MSB-first)
+    uint32_t cslot;        // words per tile's code stream
+    uint32_t k;            // bases per record = n + k - 1
 };
 inline RecSrc dense_src(const uint64_t *rec, uint64_t nrec, int W) {
-    return RecSrc{rec, nullptr, nrec, (nrec + PART_TILE - 1) / PART_TILE, PART_TILE, (uint32_t)W, nullptr};
+    return RecSrc{rec, nullptr, nrec, (nrec + PART_TILE - 1) / PART_TILE, PART_TILE, (uint32_t)W,
+                  nullptr, nullptr, nullptr, 0u, 0u};
 }
-inline RecSrc tiled_src(const uint64_t *rec, const uint32_t *tcnt, uint64_t nrec, uint64_t ntiles, uint32_t tcap,
-                        int W, const uint32_t *hdr = nullptr) {
-    return RecSrc{rec, tcnt, nrec, ntiles, tcap, (uint32_t)W, hdr};
+inline RecSrc tiled_src(const uint32_t *hdr, const uint16_t *pos, const uint32_t *code, const uint32_t *tcnt,
+                        uint64_t nrec, uint64_t ntiles, uint32_t tcap, uint32_t cslot, int W, int k) {
+    return RecSrc{nullptr, tcnt, nrec, ntiles, tcap, (uint32_t)W, hdr, pos, code, cslot, (uint32_t)k};
 }
 
 // ---- partition records by part = (bin % G) [dest] or (bin / G) [local bin]
