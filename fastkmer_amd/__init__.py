@@ -135,6 +135,8 @@ def lib():
         "fk_comm_init_local": (ctypes.c_int, [P, I32]),
         "fk_comm_transport": (ctypes.c_char_p, [P]),
         "fk_exchange_plan": (ctypes.c_int, [I32, I32, P, P, U64, P, P, P, P, P]),
+        "fk_debug_wave_count": (ctypes.c_int, [I32, I32, I32, ctypes.c_uint32, ctypes.c_uint32, I32, P,
+                                               ctypes.c_uint32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -438,6 +440,21 @@ class KmerCounter:
         st = fk_stats()
         _check(lib().fk_get_stats(self._h, ctypes.byref(st)))
         return {n: getattr(st, n) for n, _ in fk_stats._fields_}
+
+
+def debug_wave_count(keys: np.ndarray, k: int, F: int, c0: int, c1: int, slots: int, device: int = 0):
+    """Test hook (fk_debug_wave_count): one bucket of keys (uint64; (hi, lo) rows
+    for k > 32) through the wave-tier count kernel; returns (distinct keys, counts)."""
+    kw = 1 if k <= 32 else 2
+    keys = np.ascontiguousarray(keys, dtype=np.uint64).reshape(-1, kw)
+    n = len(keys)
+    ok = np.zeros(n * kw, dtype=np.uint64)
+    oc = np.zeros(n, dtype=np.uint32)
+    nout = ctypes.c_uint32(0)
+    _check(lib().fk_debug_wave_count(device, k, F, c0, c1, slots, keys.ctypes.data, n, ok.ctypes.data,
+                                     oc.ctypes.data, ctypes.byref(nout)))
+    u = nout.value
+    return (ok[:u] if kw == 1 else ok[:2 * u].reshape(-1, 2)), oc[:u]
 
 
 def comm_unique_id() -> bytes:

@@ -336,6 +336,8 @@ struct fk_ctx {
     bool pieces_void = false;     // a fallback or a retract: the pieces are counted again at the end
     bool count_pieces = true;     // FASTKMER_PIECE_COUNT=0: count the whole input in fk_finish
     uint64_t tiles_counted = 0;   // one rank: tiled records [0, tiles_counted) counted
+    uint64_t job_bytes = 0;       // one rank: the job's input size when one fk_ingest call holds it all (0: streamed)
+    std::vector<double> piece_cuts{0.55};  // FASTKMER_PIECE_CUTS: piece ends as fractions of job_bytes
     size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) counted
     double acc_ms_part = 0.0, acc_ms_count = 0.0, acc_ms_merge = 0.0;  // the job's earlier pieces
     DevBuf m2_bin_tile0, m2_split_a, m2_split_b, m2_bnd, m2_tcount, m2_toff, m2_keys, m2_counts;
@@ -513,6 +515,16 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         c->piece_bytes_set = true;
     }
     if (const char *pc = getenv("FASTKMER_PIECE_COUNT"); pc && pc[0]) c->count_pieces = atoi(pc) != 0;
+    if (const char *pc = getenv("FASTKMER_PIECE_CUTS"); pc && pc[0]) {  // e.g. "0.6" or "0.5,0.8"
+        c->piece_cuts.clear();
+        for (const char *q = pc; *q;) {
+            char *e = nullptr;
+            const double f = strtod(q, &e);
+            if (e == q) break;
+            if (f > 0.0 && f < 1.0) c->piece_cuts.push_back(f);
+            q = *e == ',' ? e + 1 : e;
+        }
+    }
     if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
         c->ingest_seg = std::max(1ull << 16, strtoull(sg, nullptr, 10));
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -761,6 +773,7 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     // with a communicator, every piece of mapped tiles is exchanged while later ones land
     const bool pieces = c->comm && c->pm_active;
     if (pieces && fresh) c->xch.expect_bytes = last ? n : 0;
+    if (fresh) c->job_bytes = last ? n : 0;
     HIP_TRY(hipEventRecord(c->h2d_ev[0], cs));
     if (pinned) {
         // every segment's copy is queued first, so the DMA runs back to back even while the
@@ -1972,10 +1985,24 @@ static void finish_pieces(fk_ctx *c, bool merged_last) {
 
 // One rank: counts the tiles mapped since the last piece once they cover a piece (fk_ingest).
 // The fused map's fallback flag is read first: a flagged input is counted whole by fk_finish.
+// Piece ends: with the job's size known (one fk_ingest call) and no FASTKMER_PIECE_BYTES, at the
+// fractions piece_cuts of it (default one cut at 55 %: the first piece's count runs while the rest
+// lands, and the last piece -- counted and merged after the last byte lands -- is the smaller one);
+// jobs under 2 * MIN_PIECE are counted whole.  A streamed job: every piece_bytes.
+static bool local_piece_due(const fk_ctx *c) {
+    constexpr uint64_t MIN_PIECE = 256ull << 20;
+    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    if (c->job_bytes && !c->piece_bytes_set) {
+        if (c->job_bytes < 2 * MIN_PIECE || c->npieces >= c->piece_cuts.size()) return false;
+        const uint64_t end = (uint64_t)(c->piece_cuts[c->npieces] * (double)c->job_bytes);
+        return c->pm_tiles * tile >= end && (c->pm_tiles - c->tiles_counted) * tile >= MIN_PIECE / 2;
+    }
+    return (c->pm_tiles - c->tiles_counted) * tile >= c->piece_bytes;
+}
+
 static int local_maybe_piece(fk_ctx *c) {
     if (!piece_counting(c)) return FK_OK;
-    const uint64_t tile = fm_tile_bytes(c->fused_nt);
-    if ((c->pm_tiles - c->tiles_counted) * tile < c->piece_bytes) return FK_OK;
+    if (!local_piece_due(c)) return FK_OK;
     uint64_t h[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2406,6 +2433,56 @@ FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *count
         HIP_TRY(hipMemcpy(keys, c->dense_keys.as<uint64_t>() + b0 * c->KW, cnt * 8 * c->KW, hipMemcpyDeviceToHost));
     if (counts) HIP_TRY(hipMemcpy(counts, c->dense_counts.as<uint32_t>() + b0, cnt * 4, hipMemcpyDeviceToHost));
     return FK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// test hook: one bucket through the wave tier (k_bucket_count64_wave / k_bucket_count128_wave)
+// ---------------------------------------------------------------------------
+FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t c0, uint32_t c1, int32_t slots,
+                                  const uint64_t *keys, uint32_t n, uint64_t *out_keys, uint32_t *out_counts,
+                                  uint32_t *n_out) {
+    if (!keys || !out_keys || !out_counts || !n_out || k < 1 || k > 63 || F < 1 || F > MAX_FINE_BITS || c1 <= c0 ||
+        c1 > (1u << F))
+        return set_err(FK_E_INVALID, "bad argument");
+    const int KW = k <= 32 ? 1 : 2;
+    const uint32_t cap = KW == 1 ? WAVE_BUCKET_CAP : WAVE128_BUCKET_CAP;
+    if (n == 0 || n > cap) return set_err(FK_E_RANGE, "a wave bucket holds 1..%u keys", cap);
+    const bool small = KW == 1 ? slots == 768 : slots == 384;
+    if (!(KW == 1 ? (slots == 768 || slots == 1024) : (slots == 384 || slots == 512)))
+        return set_err(FK_E_INVALID, "slots: 768 / 1024 (k <= 32), 384 / 512 (k > 32)");
+    const int sh = 2 * k - F;
+    for (uint32_t i = 0; i < n; ++i) {  // every key inside the bucket's cells
+        const uint64_t hi = KW == 1 ? 0 : keys[2 * i], lo = KW == 1 ? keys[i] : keys[2 * i + 1];
+        const uint64_t cell = sh >= 64 ? (hi >> (sh - 64)) : (sh == 0 ? lo : ((hi << (64 - sh)) | (lo >> sh)));
+        if ((KW == 1 && k < 32 && (lo >> (2 * k)) != 0) || cell < c0 || cell >= c1)
+            return set_err(FK_E_RANGE, "key %u lies outside cells [%u, %u)", i, c0, c1);
+    }
+    DeviceGuard dg_(device);
+    DevBuf dk, dok, doc, du, db;
+    FK_TRY(ensure(dk, (uint64_t)n * 8 * KW));
+    FK_TRY(ensure(dok, (uint64_t)n * 8 * KW));
+    FK_TRY(ensure(doc, (uint64_t)n * 4));
+    FK_TRY(ensure(du, 16));
+    FK_TRY(ensure(db, sizeof(Bucket)));
+    const Bucket b{0, n, 0, c0, c1};
+    int rc = FK_OK;
+    hipError_t e = hipMemcpy(dk.p, keys, (uint64_t)n * 8 * KW, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(db.p, &b, sizeof(Bucket), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = KW == 1 ? launch_bucket_count64_wave(dk.as<uint64_t>(), F, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
+                                                 doc.as<uint32_t>(), du.as<uint64_t>(), 1, WAVE_BUCKET_CAP,
+                                                 (uint32_t)slots, nullptr, nullptr)
+                    : launch_bucket_count128_wave(dk.as<uint64_t>(), F, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
+                                                  doc.as<uint32_t>(), du.as<uint64_t>(), small, nullptr);
+    uint64_t U = 0;
+    if (e == hipSuccess) e = hipMemcpy(&U, du.p, 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && U <= n) e = hipMemcpy(out_keys, dok.p, U * 8 * KW, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && U <= n) e = hipMemcpy(out_counts, doc.p, U * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = set_err(FK_E_DEVICE, "%s", hipGetErrorString(e));
+    else if (U > n) rc = set_err(FK_E_INVALID, "bucket reported %llu distinct keys of %u", (unsigned long long)U, n);
+    *n_out = (uint32_t)U;
+    release(dk), release(dok), release(doc), release(du), release(db);
+    return rc;
 }
 
 FK_EXPORT int fk_get_stats(fk_ctx *c, fk_stats *out) {

@@ -222,6 +222,18 @@ int fk_get_bin(fk_ctx *ctx, int32_t bin, uint64_t *keys, uint32_t *counts, size_
 int fk_write_bins(fk_ctx *ctx, const char *out_dir);
 int fk_get_stats(fk_ctx *ctx, fk_stats *out);
 
+/* ---- test hook (no reference counterpart) ----
+ * One bucket through the wave-tier count kernel on `device`: the n keys
+ * (k <= 32: one word each, n <= 512; 33 <= k <= 63: (hi, lo) pairs, n <= 256)
+ * must lie in cells [c0, c1) of F cell bits (cell = top F bits of the 2k-bit
+ * key); slots = table slots per bucket (768 / 1024, or 384 / 512 for k > 32).
+ * Writes the distinct keys ascending and their counts, *n_out of them.  Lets
+ * tests drive adversarial buckets (every key in one rank group, keys over all
+ * groups) that FASTA inputs cannot aim at. */
+int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t c0, uint32_t c1, int32_t slots,
+                        const uint64_t *keys, uint32_t n, uint64_t *out_keys, uint32_t *out_counts,
+                        uint32_t *n_out);
+
 /* ---- bin-signature diagnostics (executeFindBinSignaturesJob, SBKC:956-986) ----
  * fk_signature_counts: after the final fk_ingest (the input is left in place,
  *   fk_map may follow), d_counts[v] (device memory of the ctx device, uint64)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 3 (b): fused/parity/pieces GPU tests, then the bench and a kernel-stats profile of the bench
+# GPU tests (FK_TESTS, default fused/parity/pieces; set it inside the gpurun command), the bench and
+# a kernel-trace profile of the bench (gpurun_out/q_*): gpurun -- "FK_TESTS=... bash scripts/quick.sh"
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out
