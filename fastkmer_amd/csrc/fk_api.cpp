@@ -191,6 +191,12 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// FASTKMER_HOST_TRACE=1: host timestamps of the count's steps on stderr (where the GPU waits on the host)
+static void htrace(const char *what) {
+    static const bool on = getenv("FASTKMER_HOST_TRACE") && getenv("FASTKMER_HOST_TRACE")[0] == '1';
+    if (on) fprintf(stderr, "htrace %.3f %s\n", now_ms(), what);
+}
+
 // Every exported call that touches the GPU selects the context's device for
 // its duration and restores the caller's current device on return, so one
 // thread may drive contexts on several GPUs and a context may move between
@@ -1367,6 +1373,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     uint64_t nbuckets = 0;
     HIP_TRY(hipMemcpyAsync(&nbuckets, c->flag_scan.as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    htrace("sorted: nbuckets read");
     FK_TRY(ensure(c->buckets, nbuckets * sizeof(Bucket)));
     FK_TRY(ensure(c->out_keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->out_counts, total_kmers * 4));
@@ -1398,6 +1405,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         uint32_t ntier[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+    htrace("sorted: tiers read");
         if (ntier[0] && c->KW == 1)
             HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[0], k,
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
@@ -1454,6 +1462,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     uint64_t distinct = 0;
     HIP_TRY(hipMemcpyAsync(&distinct, c->dense_off.as<uint64_t>() + nbuckets, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    htrace("sorted: distinct read");
     FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
     FK_TRY(ensure(c->dense_counts, distinct * 4));
     FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
@@ -1698,6 +1707,7 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
     HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memcpy(c->h_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
+    htrace("tail: bin offsets read");
     c->stats.records_received = nrecv;
     c->stats.distinct = c->distinct;
     c->stats.ms_partition = ev_ms(c->ev[4], c->ev[5]);
@@ -1732,6 +1742,7 @@ static int reduce_src(fk_ctx *c, const RecSrc &src) {
     const uint32_t nlb = c->nlb;
     HIP_TRY(hipEventRecord(c->ev[4], s));
     FK_TRY(part_count(c->part, src, 1, c->G, local_table(c), nlb, c->ws, s));
+    htrace("reduce_src: part_count queued");
     std::vector<uint64_t> brec(nlb), bkm(nlb);
     if (c->pin_down.ensure((size_t)nlb * 16 + 16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
     if (nlb) {
@@ -1743,6 +1754,7 @@ static int reduce_src(fk_ctx *c, const RecSrc &src) {
         memcpy(brec.data(), c->pin_down.p, nlb * 8);
         memcpy(bkm.data(), c->pin_down.as<uint64_t>() + nlb, nlb * 8);
     }
+    htrace("reduce_src: part counts read");
     // record offsets per local bin after the partition
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
     uint64_t off = 0;
@@ -1759,7 +1771,9 @@ static int reduce_src(fk_ctx *c, const RecSrc &src) {
     build_chunks(nlb, ranges, chunks, bcb);
     FK_TRY(ensure(c->precs, nrecv * c->W * 8));
     FK_TRY(upload_chunks(c, chunks, bcb));
+    htrace("reduce_src: chunks uploaded");
     FK_TRY(part_scatter(c->part, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
+    htrace("reduce_src: scatter queued");
     HIP_TRY(hipEventRecord(c->ev[5], s));
     c->rsrc = c->precs.as<uint64_t>();
     return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
@@ -1893,6 +1907,7 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
     const uint32_t nlb = c->nlb;
     const double t0 = now_ms();
     // every bin's first tile (bins have ceil(n / MERGE_TILE) >= 1 tiles), staged in pinned memory
+    htrace("merge2: enter");
     if (c->pin_merge.ensure(((size_t)nlb + 1) * 4)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
     uint32_t *bin_tile0 = c->pin_merge.as<uint32_t>();
     uint64_t ntiles = 0;
@@ -1919,6 +1934,7 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
     FK_TRY(ensure(c->m2_keys, ntiles * MERGE_TILE * 8 * c->KW));
     FK_TRY(ensure(c->m2_counts, ntiles * MERGE_TILE * 4));
     HIP_TRY(hipMemcpyAsync(c->m2_bin_tile0.p, bin_tile0, ((uint64_t)nlb + 1) * 4, hipMemcpyHostToDevice, s));
+    htrace("merge2: launching");
     HIP_TRY(launch_merge2(c->KW, merge_src(a.keys, a.counts, a.bin_off), merge_src(b.keys, b.counts, b.bin_off),
                           c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles,
                           c->m2_split_a.as<uint64_t>(), c->m2_split_b.as<uint64_t>(), c->m2_bnd.as<uint64_t>(),
@@ -1928,6 +1944,7 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
     uint64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, c->m2_toff.as<uint64_t>() + ntiles, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    htrace("merge2: total read");
     FK_TRY(ensure(okeys, total * 8 * c->KW));
     FK_TRY(ensure(ocounts, total * 4));
     FK_TRY(ensure(obin_off, ((uint64_t)nlb + 1) * 8));
@@ -1942,6 +1959,7 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
     HIP_TRY(hipStreamSynchronize(s));
     memcpy(oh_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
     *odistinct = oh_bin_off[nlb];
+    htrace("merge2: bin offsets read");
     c->acc_ms_merge += ev_ms(c->ev[6], c->ev[7]);
     c->stats.ms_total += now_ms() - t0;
     return FK_OK;
@@ -1952,6 +1970,7 @@ static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &
 // the context's result buffers: the job's result.
 template <class F>
 static int count_piece(fk_ctx *c, F count, bool last) {
+    htrace("count_piece: enter");
     swap_result(c, c->tmp);
     const int rc = count();
     swap_result(c, c->tmp);
@@ -2306,6 +2325,7 @@ static int finish_exchange(fk_ctx *c) {
 }
 
 FK_EXPORT int fk_finish(fk_ctx *c) {
+    htrace("fk_finish: enter");
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     if (c->comm) {
         DeviceGuard dg_(c->device);
