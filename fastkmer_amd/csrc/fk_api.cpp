@@ -223,6 +223,14 @@ struct DeviceGuard {
 
 constexpr uint32_t CHUNK_RECORDS = 16384;  // records per expansion workgroup (never spans two bins)
 
+// The sorted count's shape: cell bits F (super-cells of 2^F2 cells), tiers.
+struct SortedPlan {
+    int F = 1, F2 = 0, F1 = 1;
+    bool tiered = false, two_level = false;
+    uint32_t cap = 2048, wave_cap = WAVE_BUCKET_CAP;
+    uint64_t max_bin = 0;  // the largest bin's k-mers the plan was made for
+};
+
 }  // namespace
 
 struct fk_ctx {
@@ -348,6 +356,19 @@ struct fk_ctx {
     size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) counted
     double acc_ms_part = 0.0, acc_ms_count = 0.0, acc_ms_merge = 0.0;  // the job's earlier pieces
     DevBuf m2_bin_tile0, m2_split_a, m2_split_b, m2_bnd, m2_tcount, m2_toff, m2_keys, m2_counts;
+    // staged pieces (one rank, sorted count, k <= 32; FASTKMER_PIECE_MODE=1, the default): each
+    // piece is partitioned and expanded into its own key array while later pieces land; the job's
+    // buckets are counted once over every piece's keys (no per-piece count, no merge)
+    int piece_mode = 1;                          // FASTKMER_PIECE_MODE: 1 staged, 0 count + merge per piece
+    std::vector<double> st_cuts{0.45, 0.7, 0.85};  // piece ends of a staged job (FASTKMER_PIECE_CUTS)
+    bool st_cuts_set = false;
+    double st_one_level = 0.2;                   // FASTKMER_STAGED_ONE_LEVEL: one-pass expansion below this job fraction
+    uint32_t st_np = 0;                          // pieces expanded in the current job
+    SortedPlan st_plan;                          // the job's cells (fixed by its first piece)
+    uint64_t st_kmers = 0;                       // k-mers expanded so far
+    DevBuf st_keys[STAGE_MAXP], st_cb[STAGE_MAXP], st_total, gathered, piece_starts;
+    int st_starts = 1;                           // FASTKMER_STAGED_STARTS=0: the wave tier reads st_cb itself
+    hipEvent_t st_ev[4 * STAGE_MAXP] = {};       // per piece: partition begin / end, expansion begin / end
 
     fk::Comm *comm = nullptr;
     hipStream_t comm_stream = nullptr;
@@ -531,7 +552,13 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
             if (f > 0.0 && f < 1.0) c->piece_cuts.push_back(f);
             q = *e == ',' ? e + 1 : e;
         }
+        c->st_cuts = c->piece_cuts;
+        if (c->st_cuts.size() > STAGE_MAXP - 1) c->st_cuts.resize(STAGE_MAXP - 1);
+        c->st_cuts_set = true;
     }
+    if (const char *pm = getenv("FASTKMER_PIECE_MODE"); pm && pm[0]) c->piece_mode = atoi(pm);
+    if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
+    if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
     if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
         c->ingest_seg = std::max(1ull << 16, strtoull(sg, nullptr, 10));
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -568,6 +595,13 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         return set_err(FK_E_DEVICE, "copy stream / events: %s", hipGetErrorString(e));
     }
     for (auto &ev : c->ev) {
+        e = hipEventCreate(&ev);
+        if (e != hipSuccess) {
+            fk_destroy(c);
+            return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
+        }
+    }
+    for (auto &ev : c->st_ev) {
         e = hipEventCreate(&ev);
         if (e != hipSuccess) {
             fk_destroy(c);
@@ -625,6 +659,12 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->ws.ptr) (void)hipFree(c->ws.ptr);
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto &ev : c->st_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (int p = 0; p < STAGE_MAXP; ++p) release(c->st_keys[p]), release(c->st_cb[p]);
+    release(c->st_total);
+    release(c->gathered);
+    release(c->piece_starts);
     if (c->seg_ev) (void)hipEventDestroy(c->seg_ev);
     for (auto &ev : c->h2d_ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1251,8 +1291,8 @@ FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_
 // reduce side
 // ---------------------------------------------------------------------------
 
-static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint64_t max_bin_kmers) {
-    hipStream_t s = c->stream;
+static SortedPlan sorted_plan(const fk_ctx *c, uint64_t max_bin_kmers) {
+    SortedPlan pl;
     const int k = c->cfg.k;
     const uint32_t cap = 2048;  // keys per LDS bucket (k_bucket_count64 / 128-bit k_bucket_sort)
     // cell bits: the largest bin's cells average cap/4 keys (a bucket groups a
@@ -1268,18 +1308,30 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     if (!two_level) F = std::min(F, MAX_FINE_BITS - 1);  // one-level scatter: 8 << F bytes of LDS <= 128 KB
     F = std::min(F, 2 * k);
-    const uint32_t ncell = 1u << F;
-    const uint64_t ncell_all = (uint64_t)c->nlb << F;
     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
     // cells per super-cell: 2^5 up to F = 13, 2^6 above (measured at configs[1] and at 8x larger bins)
     const uint32_t wave_cap = c->KW == 1 ? c->wave_cap : WAVE128_BUCKET_CAP;
     const int F2 = std::min(F, c->f2_bits >= 0 ? c->f2_bits : std::max(5, std::min(6, F - 8))), F1 = F - F2;
-    FK_TRY(ensure(c->keys, total_kmers * 8 * c->KW));
+    pl.F = F, pl.F2 = F2, pl.F1 = F1, pl.tiered = tiered, pl.two_level = two_level, pl.cap = cap, pl.wave_cap = wave_cap;
+    pl.max_bin = max_bin_kmers;
+    return pl;
+}
+
+// 4: expand the records (chunk table at c->chunks, records at c->rsrc) into canonical k-mers laid
+// out bin-major by cell in `keys`; c->cell_total = the cell totals, `cell_base` their exclusive
+// scan (ncell_all + 1 entries)
+static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint64_t total_kmers, DevBuf &keys,
+                         DevBuf &cell_base_buf) {
+    hipStream_t s = c->stream;
+    const int k = c->cfg.k;
+    const int F = pl.F, F2 = pl.F2, F1 = pl.F1;
+    const bool two_level = pl.two_level;
+    const uint32_t ncell = 1u << F;
+    const uint64_t ncell_all = (uint64_t)c->nlb << F;
+    FK_TRY(ensure(keys, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->cell_total, ncell_all * 8));
-    FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
-    FK_TRY(ensure(c->flags, ncell_all * 4));
-    FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
-    FK_TRY(ensure(c->misc, 64));
+    FK_TRY(ensure(cell_base_buf, (ncell_all + 1) * 8));
+    uint64_t *const cell_base = cell_base_buf.as<uint64_t>();
     // 4: expand records -> canonical k-mers, laid out bin-major by cell
     if (two_level) {
         // cell totals by atomics, per-chunk counts only per super-cell
@@ -1333,8 +1385,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F, c->lp.as<uint32_t>(),
                                    c->cell_total.as<uint64_t>(), s));
     }
-    HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
-                              c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
+    HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), cell_base, ncell_all, cell_base + ncell_all, c->ws, s));
     if (getenv("FASTKMER_DEBUG_CELL_SIZES")) {  // key-weighted histogram of log2(cell size), stderr
         std::vector<uint64_t> ct(ncell_all);
         HIP_TRY(hipMemcpyAsync(ct.data(), c->cell_total.p, ncell_all * 8, hipMemcpyDeviceToHost, s));
@@ -1351,13 +1402,31 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     if (two_level) {
         FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
         HIP_TRY(launch_expand_two_level(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
-                                        F2, c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->mid.as<uint64_t>(),
-                                        c->keys.as<uint64_t>(), s, c->x2_l1));
+                                        F2, c->lp.as<uint32_t>(), cell_base, c->mid.as<uint64_t>(),
+                                        keys.as<uint64_t>(), s, c->x2_l1));
     } else {
         HIP_TRY(launch_expand_scatter(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,
-                                      c->lp.as<uint32_t>(), c->cell_base.as<uint64_t>(), c->keys.as<uint64_t>(),
-                                      max_bin_kmers < (1ull << 31) ? c->scatter_wc : 0, s));
+                                      c->lp.as<uint32_t>(), cell_base, keys.as<uint64_t>(),
+                                      pl.max_bin < (1ull << 31) ? c->scatter_wc : 0, s));
     }
+    return FK_OK;
+}
+
+// 4c + 5: buckets over c->cell_total / c->cell_base (the job's cells), their exact counts from
+// `src` (one key array, or the staged pieces'), the dense result and its bin offsets
+static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in, uint64_t total_kmers) {
+    hipStream_t s = c->stream;
+    const int k = c->cfg.k;
+    const int F = pl.F;
+    const bool tiered = pl.tiered;
+    const uint32_t cap = pl.cap, wave_cap = pl.wave_cap;
+    const uint64_t ncell_all = (uint64_t)c->nlb << F;
+    FK_TRY(ensure(c->flags, ncell_all * 4));
+    FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
+    FK_TRY(ensure(c->misc, 64));
+    // the streaming radix path reads one contiguous array: the staged pieces' large buckets are
+    // gathered into c->gathered first
+    const uint64_t *flat_keys = src_in.keys;
     // 4c: buckets.  Tiered (k <= 32): cells packed greedily into buckets of
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
@@ -1381,6 +1450,12 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
     HIP_TRY(launch_bucket_write(c->cell_base.as<uint64_t>(), c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(),
                                 c->nlb, F, nbuckets, total_kmers, c->buckets.as<Bucket>(), s));
+    BucketSrc src = src_in;
+    if (src.np > 0 && c->st_starts) {  // the staged pieces' starts per bucket, read by the wave tier
+        FK_TRY(ensure(c->piece_starts, nbuckets * sizeof(PieceStarts)));
+        HIP_TRY(launch_bucket_pieces(src, c->buckets.as<Bucket>(), nbuckets, c->piece_starts.as<PieceStarts>(), s));
+        src.starts = c->piece_starts.as<PieceStarts>();
+    }
     // 5: exact count per bucket in LDS; buckets that do not fit take the streaming path
     const uint32_t small_limit = c->force_large ? 0u : cap;
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
@@ -1393,12 +1468,12 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
                                     c->bucket_unique.as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
-            HIP_TRY(launch_bucket_count64_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_count64_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
                                                c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                                c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
                                                nullptr, s));
         else
-            HIP_TRY(launch_bucket_count128_wave(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_count128_wave(src.keys, F, c->buckets.as<Bucket>(), nbuckets, k,
                                                 c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                                 c->bucket_unique.as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
                                                 s));
@@ -1407,19 +1482,19 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         HIP_TRY(hipStreamSynchronize(s));
     htrace("sorted: tiers read");
         if (ntier[0] && c->KW == 1)
-            HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[0], k,
+            HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), ntier[0], k,
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
                                           cap, 99, lists, s));
         else if (ntier[0])
-            HIP_TRY(launch_bucket_sort(2, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[0], k,
+            HIP_TRY(launch_bucket_sort(2, src.keys, c->buckets.as<Bucket>(), ntier[0], k,
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, s));
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
             // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
-            HIP_TRY(launch_bucket_count64_big(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), ntier[1], k,
+            HIP_TRY(launch_bucket_count64_big(src, c->buckets.as<Bucket>(), ntier[1], k,
                                               c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                               c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
                                               lists + nbuckets, s));
@@ -1428,20 +1503,27 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         }
         if (nlarge) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), ntier[1], k,
+            if (src.np > 0) {
+                FK_TRY(ensure(c->gathered, total_kmers * 8 * c->KW));
+                HIP_TRY(launch_bucket_gather(src, c->buckets.as<Bucket>(), lists + nbuckets, ntier[1],
+                                             c->gathered.as<uint64_t>(), s));
+                flat_keys = c->gathered.as<uint64_t>();
+            }
+            HIP_TRY(launch_bucket_sort_large(c->KW, flat_keys, c->buckets.as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              lists + nbuckets, s));
         }
         c->stats.oversize_buckets = nlarge;
     } else {
+        if (src.np > 0) return set_err(FK_E_INVALID, "staged pieces need the tiered count");
         if (c->KW == 1)
-            HIP_TRY(launch_bucket_count64(c->keys.as<uint64_t>(), F, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), nbuckets, k,
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
                                           small_limit, c->dbg_phase, nullptr, s));
         else
-            HIP_TRY(launch_bucket_sort(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_sort(c->KW, src.keys, c->buckets.as<Bucket>(), nbuckets, k,
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
                                        small_limit, nullptr, s));
@@ -1451,7 +1533,7 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
         c->stats.oversize_buckets = oversize;
         if (oversize) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            HIP_TRY(launch_bucket_sort_large(c->KW, c->keys.as<uint64_t>(), c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_sort_large(c->KW, src.keys, c->buckets.as<Bucket>(), nbuckets, k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              nullptr, s));
@@ -1473,6 +1555,13 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
                                c->bin_off.as<uint64_t>(), s));
     c->distinct = distinct;
     return FK_OK;
+}
+
+static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint64_t max_bin_kmers) {
+    const SortedPlan pl = sorted_plan(c, max_bin_kmers);
+    FK_TRY(sorted_expand(c, pl, nchunks, total_kmers, c->keys, c->cell_base));
+    BucketSrc src{c->keys.as<uint64_t>(), pl.F};
+    return sorted_count(c, pl, src, total_kmers);
 }
 
 // Hash count in LDS tables (fk_count_lds.inc): bins split into 2^f_b groups by
@@ -1733,17 +1822,18 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     return FK_OK;
 }
 
-// reduce of the records of `src` (all owned by this rank): partition by local bin, then count
-static int reduce_src(fk_ctx *c, const RecSrc &src) {
-    uint64_t nrecv = src.nrec;  // tiled sources: an upper bound, the partition counts them
-    const double t0 = now_ms();
+// partition of the records of `src` (all owned by this rank) by local bin into c->precs (the
+// count stage reads them at c->rsrc), the chunk table uploaded; bkm = k-mers per local bin
+static int partition_src(fk_ctx *c, const RecSrc &src, uint64_t &nrecv, std::vector<Chunk> &chunks,
+                         std::vector<uint32_t> &bcb, std::vector<uint64_t> &bkm, hipEvent_t e0, hipEvent_t e1) {
+    nrecv = src.nrec;  // tiled sources: an upper bound, the partition counts them
     hipStream_t s = c->stream;
-    c->have_result = false;
     const uint32_t nlb = c->nlb;
-    HIP_TRY(hipEventRecord(c->ev[4], s));
+    HIP_TRY(hipEventRecord(e0, s));
     FK_TRY(part_count(c->part, src, 1, c->G, local_table(c), nlb, c->ws, s));
     htrace("reduce_src: part_count queued");
-    std::vector<uint64_t> brec(nlb), bkm(nlb);
+    std::vector<uint64_t> brec(nlb);
+    bkm.assign(nlb, 0);
     if (c->pin_down.ensure((size_t)nlb * 16 + 16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
     if (nlb) {
         HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->part.rec.p, nlb * 8, hipMemcpyDeviceToHost, s));
@@ -1766,16 +1856,26 @@ static int reduce_src(fk_ctx *c, const RecSrc &src) {
     if (off != nrecv)
         return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
                        (unsigned long long)off, (unsigned long long)nrecv);
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> bcb;
     build_chunks(nlb, ranges, chunks, bcb);
     FK_TRY(ensure(c->precs, nrecv * c->W * 8));
     FK_TRY(upload_chunks(c, chunks, bcb));
     htrace("reduce_src: chunks uploaded");
     FK_TRY(part_scatter(c->part, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
     htrace("reduce_src: scatter queued");
-    HIP_TRY(hipEventRecord(c->ev[5], s));
+    HIP_TRY(hipEventRecord(e1, s));
     c->rsrc = c->precs.as<uint64_t>();
+    return FK_OK;
+}
+
+// reduce of the records of `src` (all owned by this rank): partition by local bin, then count
+static int reduce_src(fk_ctx *c, const RecSrc &src) {
+    const double t0 = now_ms();
+    c->have_result = false;
+    uint64_t nrecv = 0;
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    std::vector<uint64_t> bkm;
+    FK_TRY(partition_src(c, src, nrecv, chunks, bcb, bkm, c->ev[4], c->ev[5]));
     return reduce_tail(c, nrecv, chunks, bcb, bkm, t0);
 }
 
@@ -1866,6 +1966,8 @@ FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, c
 
 static void pieces_reset(fk_ctx *c) {
     c->npieces = 0;
+    c->st_np = 0;
+    c->st_kmers = 0;
     c->pieces_void = false;
     c->tiles_counted = 0;
     c->segs_counted = 0;
@@ -2003,6 +2105,95 @@ static void finish_pieces(fk_ctx *c, bool merged_last) {
     c->have_result = true;
 }
 
+// ---- staged pieces (one rank, sorted count, k <= 32)
+static bool staged_eligible(const fk_ctx *c) {
+    return c->piece_mode == 1 && c->KW == 1 && !c->cfg.use_ht && c->G == 1 && c->count_mode == 1 &&
+           c->dbg_phase == 99 && !c->force_large && c->expand_levels >= 2 &&
+           wave_staged_supported(c->wave_cap, c->wave_slots, c->wave_bpw);
+}
+
+// Partitions one piece and expands it into its own key array (st_keys[p], its cells' exclusive
+// scan in st_cb[p]); the job's cell totals accumulate in st_total.  The first piece fixes the
+// job's cells: its largest bin scaled by the job's size over the bytes mapped so far.
+static int staged_expand(fk_ctx *c, const RecSrc &src, uint64_t mapped_bytes, uint64_t piece_bytes) {
+    hipStream_t s = c->stream;
+    const uint32_t p = c->st_np;
+    if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
+    uint64_t nrecv = 0;
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    std::vector<uint64_t> bkm;
+    FK_TRY(partition_src(c, src, nrecv, chunks, bcb, bkm, c->st_ev[4 * p], c->st_ev[4 * p + 1]));
+    uint64_t pk = 0, maxb = 0;
+    for (uint64_t v : bkm) pk += v, maxb = std::max(maxb, v);
+    if (pk == 0) return FK_OK;  // nothing to expand (the piece's records hold no k-mers)
+    if (p == 0) {
+        const double scale = c->job_bytes && mapped_bytes ? std::max(1.0, (double)c->job_bytes / (double)mapped_bytes)
+                                                          : 2.0;
+        c->st_plan = sorted_plan(c, (uint64_t)((double)maxb * scale));
+        if (!c->st_plan.tiered || !c->st_plan.two_level)
+            return set_err(FK_E_STATE, "staged pieces need the tiered two-level count");
+    }
+    // a small piece (FASTKMER_STAGED_ONE_LEVEL: below this fraction of the job) is scattered to its
+    // cells in one pass: the second pass's cost per super-cell does not shrink with the piece
+    SortedPlan pl = c->st_plan;
+    if (c->job_bytes && (double)piece_bytes < c->st_one_level * (double)c->job_bytes && pl.F <= MAX_FINE_BITS - 1)
+        pl.two_level = false;
+    HIP_TRY(hipEventRecord(c->st_ev[4 * p + 2], s));
+    FK_TRY(sorted_expand(c, pl, (uint32_t)chunks.size(), pk, c->st_keys[p], c->st_cb[p]));
+    const uint64_t ncell_all = (uint64_t)c->nlb << c->st_plan.F;
+    FK_TRY(ensure(c->st_total, ncell_all * 8));
+    HIP_TRY(launch_add_u64(c->st_total.as<uint64_t>(), c->cell_total.as<uint64_t>(), ncell_all, p == 0, s));
+    HIP_TRY(hipEventRecord(c->st_ev[4 * p + 3], s));
+    c->st_kmers += pk;
+    c->st_np = p + 1;
+    htrace("staged: piece expanded");
+    return FK_OK;
+}
+
+// The job's count over the staged pieces: buckets over the summed cell totals, each bucket's keys
+// read from every piece (BucketSrc pieces), the dense result and its bin offsets.
+static int staged_count(fk_ctx *c) {
+    const double t0 = now_ms();
+    hipStream_t s = c->stream;
+    const SortedPlan pl = c->st_plan;
+    const uint32_t nlb = c->nlb;
+    const uint64_t ncell_all = (uint64_t)nlb << pl.F;
+    HIP_TRY(hipEventRecord(c->ev[6], s));
+    std::swap(c->cell_total, c->st_total);  // the job's cell totals (st_total is rebuilt by the next job)
+    FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
+    HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
+                              c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
+    BucketSrc src{nullptr, pl.F};
+    src.np = (int)c->st_np;
+    for (uint32_t p = 0; p < c->st_np; ++p) {
+        src.pk[p] = c->st_keys[p].as<uint64_t>();
+        src.pcb[p] = c->st_cb[p].as<uint64_t>();
+    }
+    FK_TRY(sorted_count(c, pl, src, c->st_kmers));
+    HIP_TRY(hipEventRecord(c->ev[7], s));
+    c->h_bin_off.assign((size_t)nlb + 1, 0);
+    if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    memcpy(c->h_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
+    htrace("staged: bin offsets read");
+    double mp = 0.0, mx = 0.0;
+    for (uint32_t p = 0; p < c->st_np; ++p) {
+        mp += ev_ms(c->st_ev[4 * p], c->st_ev[4 * p + 1]);
+        mx += ev_ms(c->st_ev[4 * p + 2], c->st_ev[4 * p + 3]);
+    }
+    c->stats.ms_partition = mp;
+    c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]);
+    c->stats.ms_merge = 0.0;
+    c->stats.pieces_counted = c->st_np;
+    c->stats.records_received = c->nrec;
+    c->stats.distinct = c->distinct;
+    c->stats.ms_total += now_ms() - t0;
+    c->have_result = true;
+    return FK_OK;
+}
+
 // One rank: counts the tiles mapped since the last piece once they cover a piece (fk_ingest).
 // The fused map's fallback flag is read first: a flagged input is counted whole by fk_finish.
 // Piece ends: with the job's size known (one fk_ingest call) and no FASTKMER_PIECE_BYTES, at the
@@ -2016,11 +2207,16 @@ static bool local_piece_due(const fk_ctx *c) {
     // merge) is paid once per piece.  Past half distinct (the last job's ratio) one count after the
     // last byte is the shorter path (configs[3] shape, 93 % distinct: 48.2 ms per GB with a piece,
     // ~42.7 without).
-    if (c->job_ratio > 0.5 && !c->piece_bytes_set) return false;
+    // Staged pieces (expanded only, counted once at the end) repeat no work: they always pay, and
+    // the last one -- expanded after the last byte lands -- is the smallest.
+    const bool staged = staged_eligible(c);
+    if (staged && c->st_np >= (uint32_t)STAGE_MAXP - 1) return false;
+    if (!staged && c->job_ratio > 0.5 && !c->piece_bytes_set) return false;
+    const std::vector<double> &cuts = staged ? c->st_cuts : c->piece_cuts;
     const uint64_t tile = fm_tile_bytes(c->fused_nt);
     if (c->job_bytes && !c->piece_bytes_set) {
-        if (c->job_bytes < 2 * MIN_PIECE || c->npieces >= c->piece_cuts.size()) return false;
-        const uint64_t end = (uint64_t)(c->piece_cuts[c->npieces] * (double)c->job_bytes);
+        if (c->job_bytes < 2 * MIN_PIECE || c->npieces >= cuts.size()) return false;
+        const uint64_t end = (uint64_t)(cuts[c->npieces] * (double)c->job_bytes);
         return c->pm_tiles * tile >= end && (c->pm_tiles - c->tiles_counted) * tile >= MIN_PIECE / 2;
     }
     return (c->pm_tiles - c->tiles_counted) * tile >= c->piece_bytes;
@@ -2039,6 +2235,11 @@ static int local_maybe_piece(fk_ctx *c) {
     const uint64_t t0 = c->tiles_counted, nt = c->pm_tiles - t0;
     const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
     c->tiles_counted = c->pm_tiles;
+    if (staged_eligible(c)) {
+        FK_TRY(staged_expand(c, src, c->pm_tiles * fm_tile_bytes(c->fused_nt), nt * fm_tile_bytes(c->fused_nt)));
+        c->npieces += 1;
+        return FK_OK;
+    }
     return count_piece(c, [&] { return reduce_src(c, src); }, false);
 }
 
@@ -2336,6 +2537,17 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
                                    "fk_map/fk_map_emit/fk_reduce", c->G);
     FK_TRY(fk_map(c, nullptr));
     DeviceGuard dg_(c->device);
+    if (c->st_np && c->rec_tiled && !c->pieces_void && c->tiles_counted <= c->rec_tiles) {
+        // staged pieces were expanded while the input landed: the last piece, then one count
+        if (c->rec_tiles > c->tiles_counted) {
+            const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
+            FK_TRY(staged_expand(c, fused_src(c, t0, nt, nt * map_fused_tcap()), 0, nt * fm_tile_bytes(c->fused_nt)));
+        }
+        FK_TRY(staged_count(c));
+        pieces_reset(c);
+        if (c->nkmers) c->job_ratio = (double)c->distinct / (double)c->nkmers;
+        return FK_OK;
+    }
     if (c->npieces && c->rec_tiled && !c->pieces_void && c->tiles_counted <= c->rec_tiles) {
         // pieces were counted while the input landed: the last piece, merged in
         const bool more = c->rec_tiles > c->tiles_counted;
@@ -2499,7 +2711,7 @@ FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t
     hipError_t e = hipMemcpy(dk.p, keys, (uint64_t)n * 8 * KW, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(db.p, &b, sizeof(Bucket), hipMemcpyHostToDevice);
     if (e == hipSuccess)
-        e = KW == 1 ? launch_bucket_count64_wave(dk.as<uint64_t>(), F, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
+        e = KW == 1 ? launch_bucket_count64_wave(BucketSrc{dk.as<uint64_t>(), F}, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
                                                  doc.as<uint32_t>(), du.as<uint64_t>(), 1, WAVE_BUCKET_CAP,
                                                  (uint32_t)slots, nullptr, nullptr)
                     : launch_bucket_count128_wave(dk.as<uint64_t>(), F, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),

@@ -40,6 +40,28 @@ struct Bucket {
     uint32_t c0, c1; // cells [c0, c1) of the bin
 };
 
+// A bucket's keys: np == 0, the contiguous range keys[begin, begin + n); np = 1..STAGE_MAXP,
+// the staged pieces' key arrays (one job's input expanded piece by piece while it landed, and
+// counted once): piece p holds the bucket's keys at pk[p][pcb[p][g0] .. pcb[p][g1]), g0 / g1 =
+// (lbin << F) + c0 / c1, pcb[p] the exclusive scan of the piece's cell totals.
+constexpr int STAGE_MAXP = 4;
+struct BucketSrc {
+    const uint64_t *keys;
+    int F;  // cell bits: a bucket's keys lie in [c0 << (2k-F), c1 << (2k-F))
+    int np = 0;
+    const uint64_t *pk[STAGE_MAXP] = {};
+    const uint64_t *pcb[STAGE_MAXP] = {};
+    const struct PieceStarts *starts = nullptr;  // per bucket (launch_bucket_pieces), or null
+};
+// one bucket's keys in the staged pieces: piece p's first key at s[p] of pk[p], pre[p] keys of
+// the bucket in the pieces before p (pre[p] = ~0u for p >= np)
+struct PieceStarts {
+    uint64_t s[STAGE_MAXP];
+    uint32_t pre[STAGE_MAXP];
+};
+hipError_t launch_bucket_pieces(const BucketSrc &src, const struct Bucket *buckets, uint64_t nb, PieceStarts *out,
+                                hipStream_t s);
+
 struct Chunk {
     uint64_t rec_begin, rec_end;  // records [begin, end) of one local bin
     uint32_t lbin, pad;
@@ -157,11 +179,11 @@ hipError_t launch_bucket_flags(const uint64_t *cell_base, const uint64_t *cell_t
 hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags, const uint64_t *flag_scan,
                                uint32_t nlbins, int F, uint64_t nbuckets, uint64_t total_keys, Bucket *buckets,
                                hipStream_t s);
-hipError_t launch_bucket_count64(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
+hipError_t launch_bucket_count64(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
                                  const uint32_t *list, hipStream_t s);
-hipError_t launch_bucket_count64_big(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nlist, int k,
+hipError_t launch_bucket_count64_big(const BucketSrc &src, const Bucket *buckets, uint64_t nlist, int k,
                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                      unsigned long long *oversize, const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
@@ -188,9 +210,16 @@ hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbin
                                       int period_bits, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
                                uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts, hipStream_t s);
-hipError_t launch_bucket_count64_wave(const uint64_t *keys, int F, const Bucket *buckets, uint64_t nbuckets, int k,
+hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique, int bpw,
                                       uint32_t wave_cap, uint32_t wave_slots, const uint32_t *list, hipStream_t s);
+// staged pieces (src.np > 0) in the wave tier: the default tier configuration only
+bool wave_staged_supported(uint32_t wave_cap, uint32_t wave_slots, int bpw);
+// keys of the listed buckets from the staged pieces to out[begin, begin + n)
+hipError_t launch_bucket_gather(const BucketSrc &src, const Bucket *buckets, const uint32_t *list, uint64_t nlist,
+                                uint64_t *out, hipStream_t s);
+// dst[i] += src[i] (dst = src when `copy`)
+hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
 hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, const uint32_t *list, hipStream_t s);

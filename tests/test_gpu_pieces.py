@@ -1,4 +1,9 @@
-"""Per-piece counts merged into a running result (fk_merge.inc), through the C-ABI.
+"""Pieces of a job counted while the FASTA is still landing, through the C-ABI.
+
+Two modes (FASTKMER_PIECE_MODE): 1, staged (the default for k <= 32): every piece is
+partitioned and expanded into its own key array, and fk_finish counts the job's
+buckets once over all the pieces' keys; 0, per-piece counts merged (fk_merge.inc,
+the k > 32 path), described below.
 
 While the FASTA is still being copied in, every landed piece of it is
 counted on its own (the sorted count of extractKXmers, SBKC:540-597, on the
@@ -21,10 +26,12 @@ from test_gpu_parity import assert_same_as_oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def small_pieces(monkeypatch):
+@pytest.fixture(params=[1, 0], ids=["staged", "merge"])
+def small_pieces(monkeypatch, request):
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(request.param))
+    return request.param
 
 
 def count_pinned(fasta, k, m, B=2048, use_ht=False, seq=0, repeat=1):
@@ -95,11 +102,54 @@ def test_piece_counts_hash_mode_counts_once(small_pieces):
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048), ordered=False)
 
 
-def test_piece_counts_many_small_pieces(monkeypatch):
-    # dozens of pieces, each merged into the running result as it is counted
+@pytest.mark.parametrize("mode", [1, 0], ids=["staged", "merge"])
+def test_piece_counts_many_small_pieces(monkeypatch, mode):
+    # merge: dozens of pieces, each merged into the running result as it is counted; staged: the
+    # first pieces expanded as they land (at most STAGE_MAXP pieces), the rest the last piece
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(64 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(64 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(mode))
     fasta = fk.synth_fasta(30_000, 100, 500_000, seed=0xA6)
     kc = count_pinned(fasta, 28, 10, repeat=2)
-    assert kc.stats()["pieces_counted"] >= 20
+    if mode:
+        assert kc.stats()["pieces_counted"] == 4
+    else:
+        assert kc.stats()["pieces_counted"] >= 20
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
+
+
+@pytest.mark.parametrize("cuts,one_level", [("0.45,0.7,0.85", "0.2"), ("0.3", "0"), ("0.2,0.25,0.97", "0.5")])
+def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level):
+    # a 1 GB job in one fk_ingest call (pinned): staged pieces at the job-size cuts (the
+    # bench's path) against the same job counted whole on the device (FASTKMER_PIECE_COUNT=0),
+    # every bin's keys and counts equal; a sampled slice of bins against the oracle is in
+    # test_gpu_write; here both GPU paths must agree on all 2048 bins (a piece ends at its cut once it
+    # holds >= 128 MB: "0.2,0.25,0.97" cuts at 0.2, ~0.33 and 0.97)
+    import torch
+    n_reads = 1_000_000_000 // 114  # BASELINE configs[1]: pieces of >= 128 MB at every cut below
+    dev = torch.empty(n_reads * 114, dtype=torch.uint8, device="cuda")
+    fk.synth_fasta_to_device(dev.data_ptr(), n_reads, 100, 100_000_000, seed=0x5EED)
+    host = torch.empty(dev.numel(), dtype=torch.uint8).pin_memory()
+    host.copy_(dev)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("FASTKMER_PIECE_CUTS", cuts)
+    monkeypatch.setenv("FASTKMER_STAGED_ONE_LEVEL", one_level)  # pieces below this job fraction: one pass
+    a = fk.KmerCounter(28, 10, 3, 2048)
+    a.ingest_ptr(host.data_ptr(), host.numel())
+    a.finish()
+    st = a.stats()
+    assert st["pieces_counted"] == cuts.count(",") + 2
+    monkeypatch.setenv("FASTKMER_PIECE_COUNT", "0")
+    b = fk.KmerCounter(28, 10, 3, 2048)
+    b.ingest_device(dev.data_ptr(), dev.numel())
+    b.finish()
+    assert b.stats()["pieces_counted"] == 0
+    assert st["kmers"] == b.stats()["kmers"] and st["distinct"] == b.stats()["distinct"]
+    sa, sb = a.bin_sizes(), b.bin_sizes()
+    assert np.array_equal(sa, sb)
+    for bin_ in range(2048):
+        ka, ca = a.get_bin(bin_)
+        kb, cb = b.get_bin(bin_)
+        assert np.array_equal(ka, kb) and np.array_equal(ca, cb), f"bin {bin_}"
+    a.close()
+    b.close()
