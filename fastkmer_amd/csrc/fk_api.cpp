@@ -2105,31 +2105,28 @@ static void finish_pieces(fk_ctx *c, bool merged_last) {
     c->have_result = true;
 }
 
-// ---- staged pieces (one rank, sorted count, k <= 32)
-static bool staged_eligible(const fk_ctx *c) {
-    return c->piece_mode == 1 && c->KW == 1 && !c->cfg.use_ht && c->G == 1 && c->count_mode == 1 &&
-           c->dbg_phase == 99 && !c->force_large && c->expand_levels >= 2 &&
-           wave_staged_supported(c->wave_cap, c->wave_slots, c->wave_bpw);
+// ---- staged pieces (sorted count, k <= 32): one rank's landed pieces, or the received segments
+static bool staged_ok(const fk_ctx *c) {
+    return c->piece_mode == 1 && c->KW == 1 && !c->cfg.use_ht && c->count_mode == 1 && c->dbg_phase == 99 &&
+           !c->force_large && c->expand_levels >= 2 && wave_staged_supported(c->wave_cap, c->wave_slots, c->wave_bpw);
 }
+static bool staged_eligible(const fk_ctx *c) { return staged_ok(c) && c->G == 1 && !c->comm; }
 
 // Partitions one piece and expands it into its own key array (st_keys[p], its cells' exclusive
 // scan in st_cb[p]); the job's cell totals accumulate in st_total.  The first piece fixes the
 // job's cells: its largest bin scaled by the job's size over the bytes mapped so far.
-static int staged_expand(fk_ctx *c, const RecSrc &src, uint64_t mapped_bytes, uint64_t piece_bytes) {
+// Expands one piece's records (the chunk table at c->chunks, records at c->rsrc; bkm = k-mers per
+// local bin) into its own key array (st_keys[p], its cells' exclusive scan in st_cb[p]); the job's
+// cell totals accumulate in st_total.  `frac` = the piece's estimated fraction of the job (0:
+// unknown).  The first piece fixes the job's cells: its largest bin scaled to the job.
+static int staged_expand_chunks(fk_ctx *c, uint32_t nchunks, const std::vector<uint64_t> &bkm, double frac) {
     hipStream_t s = c->stream;
     const uint32_t p = c->st_np;
-    if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
-    uint64_t nrecv = 0;
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> bcb;
-    std::vector<uint64_t> bkm;
-    FK_TRY(partition_src(c, src, nrecv, chunks, bcb, bkm, c->st_ev[4 * p], c->st_ev[4 * p + 1]));
     uint64_t pk = 0, maxb = 0;
     for (uint64_t v : bkm) pk += v, maxb = std::max(maxb, v);
     if (pk == 0) return FK_OK;  // nothing to expand (the piece's records hold no k-mers)
     if (p == 0) {
-        const double scale = c->job_bytes && mapped_bytes ? std::max(1.0, (double)c->job_bytes / (double)mapped_bytes)
-                                                          : 2.0;
+        const double scale = frac > 0.0 ? std::max(1.0, 1.0 / frac) : 2.0;
         c->st_plan = sorted_plan(c, (uint64_t)((double)maxb * scale));
         if (!c->st_plan.tiered || !c->st_plan.two_level)
             return set_err(FK_E_STATE, "staged pieces need the tiered two-level count");
@@ -2137,10 +2134,9 @@ static int staged_expand(fk_ctx *c, const RecSrc &src, uint64_t mapped_bytes, ui
     // a small piece (FASTKMER_STAGED_ONE_LEVEL: below this fraction of the job) is scattered to its
     // cells in one pass: the second pass's cost per super-cell does not shrink with the piece
     SortedPlan pl = c->st_plan;
-    if (c->job_bytes && (double)piece_bytes < c->st_one_level * (double)c->job_bytes && pl.F <= MAX_FINE_BITS - 1)
-        pl.two_level = false;
+    if (frac > 0.0 && frac < c->st_one_level && pl.F <= MAX_FINE_BITS - 1) pl.two_level = false;
     HIP_TRY(hipEventRecord(c->st_ev[4 * p + 2], s));
-    FK_TRY(sorted_expand(c, pl, (uint32_t)chunks.size(), pk, c->st_keys[p], c->st_cb[p]));
+    FK_TRY(sorted_expand(c, pl, nchunks, pk, c->st_keys[p], c->st_cb[p]));
     const uint64_t ncell_all = (uint64_t)c->nlb << c->st_plan.F;
     FK_TRY(ensure(c->st_total, ncell_all * 8));
     HIP_TRY(launch_add_u64(c->st_total.as<uint64_t>(), c->cell_total.as<uint64_t>(), ncell_all, p == 0, s));
@@ -2149,6 +2145,18 @@ static int staged_expand(fk_ctx *c, const RecSrc &src, uint64_t mapped_bytes, ui
     c->st_np = p + 1;
     htrace("staged: piece expanded");
     return FK_OK;
+}
+
+// One rank: partitions a piece of the mapped tiles by local bin, then expands it.
+static int staged_expand(fk_ctx *c, const RecSrc &src, double frac) {
+    const uint32_t p = c->st_np;
+    if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
+    uint64_t nrecv = 0;
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    std::vector<uint64_t> bkm;
+    FK_TRY(partition_src(c, src, nrecv, chunks, bcb, bkm, c->st_ev[4 * p], c->st_ev[4 * p + 1]));
+    return staged_expand_chunks(c, (uint32_t)chunks.size(), bkm, frac);
 }
 
 // The job's count over the staged pieces: buckets over the summed cell totals, each bucket's keys
@@ -2236,8 +2244,10 @@ static int local_maybe_piece(fk_ctx *c) {
     const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
     c->tiles_counted = c->pm_tiles;
     if (staged_eligible(c)) {
-        FK_TRY(staged_expand(c, src, c->pm_tiles * fm_tile_bytes(c->fused_nt), nt * fm_tile_bytes(c->fused_nt)));
-        c->npieces += 1;
+        const uint32_t np0 = c->st_np;
+        FK_TRY(staged_expand(c, src, c->job_bytes ? (double)(nt * fm_tile_bytes(c->fused_nt)) / (double)c->job_bytes
+                                                  : 0.0));
+        if (c->st_np > np0) c->npieces += 1;  // (a piece without k-mers adds none)
         return FK_OK;
     }
     return count_piece(c, [&] { return reduce_src(c, src); }, false);
@@ -2448,6 +2458,57 @@ static int xch_count_segments(fk_ctx *c, size_t s1, bool last) {
                        last);
 }
 
+// With a communicator and staged pieces: expands the received segments [segs_counted, s1) as one
+// staged piece (they arrive grouped by local bin: no partition), once the comm stream has
+// delivered them.  `frac` = their estimated fraction of what this rank receives in the job.
+static int xch_stage_segments(fk_ctx *c, size_t s1, double frac) {
+    if (s1 <= c->segs_counted) return FK_OK;
+    const uint32_t p = c->st_np;
+    if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
+    hipStream_t s = c->stream;
+    // the chunk table goes up through the pinned staging buffer: the last upload from it is done
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t step = c->xch.segs[s1 - 1].step;
+    HIP_TRY(hipStreamWaitEvent(s, c->xev[2 * step + 1], 0));
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges;
+    std::vector<uint64_t> bkm;
+    uint64_t nrecv = 0;
+    FK_TRY(segment_ranges(c, c->segs_counted, s1, ranges, bkm, &nrecv));
+    c->segs_counted = s1;
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> bcb;
+    build_chunks(c->nlb, ranges, chunks, bcb);
+    HIP_TRY(hipEventRecord(c->st_ev[4 * p], s));
+    FK_TRY(upload_chunks(c, chunks, bcb));
+    HIP_TRY(hipEventRecord(c->st_ev[4 * p + 1], s));
+    c->rsrc = c->xrecv.as<uint64_t>();
+    return staged_expand_chunks(c, (uint32_t)chunks.size(), bkm, frac);
+}
+
+// Received records of this job so far / expected in all (estimated from the share of the input
+// sent so far; 0 when the input's size is unknown).
+static double xch_recv_frac(const fk_ctx *c, uint64_t recs) {
+    if (!c->xch.expect_bytes || !c->xch.tiles_sent || !c->xch.recv_used) return 0.0;
+    const double sent = (double)c->xch.tiles_sent * (double)fm_tile_bytes(c->fused_nt);
+    const double est = (double)c->xch.recv_used * (double)c->xch.expect_bytes / sent;
+    return est > 0.0 ? std::min(1.0, (double)recs / est) : 0.0;
+}
+
+// Staged: the segments received before this step are expanded once they hold about 1 / STAGE_MAXP
+// of the job (every step when its size is unknown), at most STAGE_MAXP - 1 times before fk_finish.
+static int xch_maybe_stage(fk_ctx *c, size_t s1) {
+    if (c->st_np >= (uint32_t)STAGE_MAXP - 1 || s1 <= c->segs_counted) return FK_OK;
+    uint64_t recs = 0;
+    for (size_t i = c->segs_counted; i < s1; ++i)
+        for (uint64_t n : c->xch.segs[i].rec) recs += n;
+    const double frac = xch_recv_frac(c, recs);
+    if (frac > 0.0 && frac < 1.0 / STAGE_MAXP) return FK_OK;
+    const uint32_t np0 = c->st_np;
+    FK_TRY(xch_stage_segments(c, s1, frac));
+    if (c->st_np > np0) c->npieces += 1;  // (segments without k-mers add no piece)
+    return FK_OK;
+}
+
 // fk_ingest: sends the tiles mapped since the last piece once they cover a piece.  The fused
 // map's fallback flag is read first: a flagged input is mapped again in fk_finish and sent
 // whole, retracting the pieces sent so far.
@@ -2468,8 +2529,11 @@ static int xch_maybe_piece(fk_ctx *c) {
     const size_t before = c->xch.segs.size();
     const int rc = xch_step(c, &src, 0);
     if (rc) return comm_fail(c, rc);
-    // the records of the earlier steps are counted while this step's are on the wire
-    if (piece_counting(c) && before > c->segs_counted) FK_TRY(xch_count_segments(c, before, false));
+    // the records of the earlier steps are counted (staged: expanded) while this step's are on the wire
+    if (piece_counting(c) && before > c->segs_counted) {
+        if (staged_ok(c)) FK_TRY(xch_maybe_stage(c, before));
+        else FK_TRY(xch_count_segments(c, before, false));
+    }
     return FK_OK;
 }
 
@@ -2500,7 +2564,16 @@ static int finish_exchange(fk_ctx *c) {
     uint64_t nrecv = 0;
     for (const auto &g : c->xch.segs)
         for (uint64_t n : g.rec) nrecv += n;
-    if (c->npieces && !c->pieces_void) {
+    if (c->st_np && !c->pieces_void) {
+        // staged: the segments not yet expanded, then one count over every piece
+        if (c->segs_counted < c->xch.segs.size()) {
+            uint64_t recs = 0;
+            for (size_t i = c->segs_counted; i < c->xch.segs.size(); ++i)
+                for (uint64_t n : c->xch.segs[i].rec) recs += n;
+            FK_TRY(xch_stage_segments(c, c->xch.segs.size(), nrecv ? (double)recs / (double)nrecv : 0.0));
+        }
+        FK_TRY(staged_count(c));
+    } else if (c->npieces && !c->pieces_void) {
         // earlier steps were counted while later ones were on the wire: the rest, merged in
         const bool more = c->segs_counted < c->xch.segs.size();
         if (more) FK_TRY(xch_count_segments(c, c->xch.segs.size(), true));
@@ -2541,7 +2614,8 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
         // staged pieces were expanded while the input landed: the last piece, then one count
         if (c->rec_tiles > c->tiles_counted) {
             const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
-            FK_TRY(staged_expand(c, fused_src(c, t0, nt, nt * map_fused_tcap()), 0, nt * fm_tile_bytes(c->fused_nt)));
+            FK_TRY(staged_expand(c, fused_src(c, t0, nt, nt * map_fused_tcap()),
+                                 c->job_bytes ? (double)(nt * fm_tile_bytes(c->fused_nt)) / (double)c->job_bytes : 0.0));
         }
         FK_TRY(staged_count(c));
         pieces_reset(c);

@@ -98,11 +98,15 @@ def assert_union_matches_oracle(ctxs, ref, ordered=True):
         assert np.array_equal(cnt, rcnt), f"counts differ in bin {b}"
 
 
-@pytest.fixture
-def small_pieces(monkeypatch):
-    # 256 KB H2D segments and 512 KB pieces: a few MB of input crosses several pieces
+@pytest.fixture(params=[1, 0], ids=["staged", "merge"])
+def small_pieces(monkeypatch, request):
+    # 256 KB H2D segments and 512 KB pieces: a few MB of input crosses several pieces; the
+    # received segments either expanded as staged pieces and counted once (1, the default for
+    # k <= 32) or counted per step and merged (0)
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(request.param))
+    return request.param
 
 
 @pytest.mark.parametrize("world,use_ht,feed", [(2, False, "pinned"), (3, False, "bytes"), (8, False, "pinned"),
