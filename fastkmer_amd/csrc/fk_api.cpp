@@ -350,7 +350,9 @@ struct fk_ctx {
     bool pieces_void = false;     // a fallback or a retract: the pieces are counted again at the end
     bool count_pieces = true;     // FASTKMER_PIECE_COUNT=0: count the whole input in fk_finish
     uint64_t tiles_counted = 0;   // one rank: tiled records [0, tiles_counted) counted
-    uint64_t job_bytes = 0;       // one rank: the job's input size when one fk_ingest call holds it all (0: streamed)
+    uint64_t job_bytes = 0;       // one rank: the job's input size when one fk_ingest call holds it all, or
+                                  // announced by fk_ingest_reserve (0: unknown)
+    uint64_t reserve_bytes = 0;   // fk_ingest_reserve's size for the next job
     std::vector<double> piece_cuts{0.55};  // FASTKMER_PIECE_CUTS: piece ends as fractions of job_bytes
     double job_ratio = -1.0;      // distinct / k-mers of the last one-rank job (-1: none yet)
     size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) counted
@@ -819,8 +821,12 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
             }
     // with a communicator, every piece of mapped tiles is exchanged while later ones land
     const bool pieces = c->comm && c->pm_active;
-    if (pieces && fresh) c->xch.expect_bytes = last ? n : 0;
-    if (fresh) c->job_bytes = last ? n : 0;
+    // the job's size: this call's when it holds the whole input, else what fk_ingest_reserve announced
+    if (pieces && fresh) c->xch.expect_bytes = last ? n : c->reserve_bytes;
+    if (fresh) {
+        c->job_bytes = last ? n : c->reserve_bytes;
+        c->reserve_bytes = 0;
+    }
     HIP_TRY(hipEventRecord(c->h2d_ev[0], cs));
     if (pinned) {
         // every segment's copy is queued first, so the DMA runs back to back even while the
@@ -882,6 +888,7 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
     DeviceGuard dg_(c->device);
     if (!c->ingest_fresh && c->d_fasta) return set_err(FK_E_STATE, "fk_ingest_reserve inside a streamed input");
     FK_TRY(ensure(c->fasta_own, total_bytes));
+    c->reserve_bytes = total_bytes;  // the next (streamed) job's size: piece cuts and staged plans follow it
     if (premap_eligible(c)) {
         const uint64_t tiles = (total_bytes + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
         FK_TRY(ensure(c->rec_hdr, tiles * map_fused_tcap() * 4));

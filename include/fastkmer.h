@@ -124,7 +124,9 @@ int fk_set_stream(fk_ctx *ctx, void *hip_stream);
 int fk_ingest(fk_ctx *ctx, const uint8_t *fasta, size_t n, int last);
 /* Optional, before a streamed fk_ingest sequence: size the device input for
  * about total_bytes, so the copies of later chunks overlap the map without a
- * reallocation (FASTdoop-style streaming ingest). */
+ * reallocation (FASTdoop-style streaming ingest).  The size also
+ * places the job's piece cuts and sizes its cells, as for a job passed in one
+ * fk_ingest call (a wrong size costs time, never results). */
 int fk_ingest_reserve(fk_ctx *ctx, uint64_t total_bytes);
 int fk_ingest_device(fk_ctx *ctx, const void *d_fasta, size_t n, int last);
 /* Fill a caller's device buffer (current device) with the same bytes as

@@ -118,8 +118,9 @@ def test_piece_counts_many_small_pieces(monkeypatch, mode):
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
 
 
-@pytest.mark.parametrize("cuts,one_level", [("0.45,0.7,0.85", "0.2"), ("0.3", "0"), ("0.2,0.25,0.97", "0.5")])
-def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level):
+@pytest.mark.parametrize("cuts,one_level,chunks", [("0.45,0.7,0.85", "0.2", 0), ("0.3", "0", 0),
+                                                   ("0.2,0.25,0.97", "0.5", 0), ("0.45,0.7,0.85", "0.2", 7)])
+def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks):
     # a 1 GB job in one fk_ingest call (pinned): staged pieces at the job-size cuts (the
     # bench's path) against the same job counted whole on the device (FASTKMER_PIECE_COUNT=0),
     # every bin's keys and counts equal; a sampled slice of bins against the oracle is in
@@ -135,7 +136,13 @@ def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level):
     monkeypatch.setenv("FASTKMER_PIECE_CUTS", cuts)
     monkeypatch.setenv("FASTKMER_STAGED_ONE_LEVEL", one_level)  # pieces below this job fraction: one pass
     a = fk.KmerCounter(28, 10, 3, 2048)
-    a.ingest_ptr(host.data_ptr(), host.numel())
+    if chunks:  # a streamed job: fk_ingest_reserve announces its size, the cuts follow it
+        a.reserve(host.numel())
+        bounds = np.linspace(0, host.numel(), chunks + 1).astype(np.int64)
+        for i in range(chunks):
+            a.ingest_ptr(host.data_ptr() + int(bounds[i]), int(bounds[i + 1] - bounds[i]), last=i == chunks - 1)
+    else:
+        a.ingest_ptr(host.data_ptr(), host.numel())
     a.finish()
     st = a.stats()
     assert st["pieces_counted"] == cuts.count(",") + 2
