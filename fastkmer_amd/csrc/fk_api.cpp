@@ -1480,7 +1480,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
                                                c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
                                                nullptr, s));
         else
-            HIP_TRY(launch_bucket_count128_wave(src.keys, F, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_count128_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
                                                 c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                                 c->bucket_unique.as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
                                                 s));
@@ -1493,11 +1493,18 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
                                           cap, 99, lists, s));
-        else if (ntier[0])
-            HIP_TRY(launch_bucket_sort(2, src.keys, c->buckets.as<Bucket>(), ntier[0], k,
+        else if (ntier[0]) {
+            if (src.np > 0) {  // the 128-bit block tier reads one contiguous array
+                FK_TRY(ensure(c->gathered, total_kmers * 8 * c->KW));
+                HIP_TRY(launch_bucket_gather(c->KW, src, c->buckets.as<Bucket>(), lists, ntier[0],
+                                             c->gathered.as<uint64_t>(), s));
+                flat_keys = c->gathered.as<uint64_t>();
+            }
+            HIP_TRY(launch_bucket_sort(2, flat_keys, c->buckets.as<Bucket>(), ntier[0], k,
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, s));
+        }
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
             // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
@@ -1512,7 +1519,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
             if (src.np > 0) {
                 FK_TRY(ensure(c->gathered, total_kmers * 8 * c->KW));
-                HIP_TRY(launch_bucket_gather(src, c->buckets.as<Bucket>(), lists + nbuckets, ntier[1],
+                HIP_TRY(launch_bucket_gather(c->KW, src, c->buckets.as<Bucket>(), lists + nbuckets, ntier[1],
                                              c->gathered.as<uint64_t>(), s));
                 flat_keys = c->gathered.as<uint64_t>();
             }
@@ -2114,8 +2121,10 @@ static void finish_pieces(fk_ctx *c, bool merged_last) {
 
 // ---- staged pieces (sorted count, k <= 32): one rank's landed pieces, or the received segments
 static bool staged_ok(const fk_ctx *c) {
-    return c->piece_mode == 1 && c->KW == 1 && !c->cfg.use_ht && c->count_mode == 1 && c->dbg_phase == 99 &&
-           !c->force_large && c->expand_levels >= 2 && wave_staged_supported(c->wave_cap, c->wave_slots, c->wave_bpw);
+    const bool tier_ok = c->KW == 1 ? wave_staged_supported(c->wave_cap, c->wave_slots, c->wave_bpw)
+                                    : c->cfg.k <= 63 && wave128_staged_supported(c->wave_slots);
+    return c->piece_mode == 1 && tier_ok && !c->cfg.use_ht && c->count_mode == 1 && c->dbg_phase == 99 &&
+           !c->force_large && c->expand_levels >= 2;
 }
 static bool staged_eligible(const fk_ctx *c) { return staged_ok(c) && c->G == 1 && !c->comm; }
 
@@ -2795,7 +2804,7 @@ FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t
         e = KW == 1 ? launch_bucket_count64_wave(BucketSrc{dk.as<uint64_t>(), F}, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
                                                  doc.as<uint32_t>(), du.as<uint64_t>(), 1, WAVE_BUCKET_CAP,
                                                  (uint32_t)slots, nullptr, nullptr)
-                    : launch_bucket_count128_wave(dk.as<uint64_t>(), F, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
+                    : launch_bucket_count128_wave(BucketSrc{dk.as<uint64_t>(), F}, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
                                                   doc.as<uint32_t>(), du.as<uint64_t>(), small, nullptr);
     uint64_t U = 0;
     if (e == hipSuccess) e = hipMemcpy(&U, du.p, 8, hipMemcpyDeviceToHost);
