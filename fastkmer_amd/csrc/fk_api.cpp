@@ -260,7 +260,7 @@ struct fk_ctx {
                                 // 128-bit keys: 384 or 512 per 256-key bucket alike)
     int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
     int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
-    int wave_bpw = 4;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4)
+    int wave_bpw = 2;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4; 2 measured fastest)
     bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
     int fused_probe = 0;       // FASTKMER_FUSED_PROBE: stop the fused map kernel after a phase (timing only)
