@@ -333,6 +333,9 @@ struct fk_ctx {
     bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
     PinBuf pin_up, pin_down, pin_merge;  // staging: chunk tables up, per-bin counts down, merge tables up
+    PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
+    hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
+    bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
 
     // multi-rank exchange inside the context (fk_comm_init / fk_comm_init_local): the input
     // is emitted in pieces grouped by (destination, local bin) and each piece is exchanged
@@ -603,6 +606,11 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
             return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
         }
     }
+    e = hipEventCreateWithFlags(&c->tier_ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        fk_destroy(c);
+        return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
+    }
     for (auto &ev : c->st_ev) {
         e = hipEventCreate(&ev);
         if (e != hipSuccess) {
@@ -640,6 +648,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->pin_up.release();
     c->pin_down.release();
     c->pin_merge.release();
+    c->pin_tier.release();
+    if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
     release(c->xsend);
     release(c->xrecv);
     for (fk_ctx::PieceRes *r : {&c->acc, &c->acc2, &c->tmp})
@@ -1473,6 +1483,11 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         uint32_t *lists = c->tier_list.as<uint32_t>();
         HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, wave_cap, cap,
                                     c->bucket_unique.as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
+        // the tier sizes go to pinned memory right behind the tier kernel: the host waits for that
+        // copy, not for the wave tier queued after it, before it queues the block tiers
+        if (c->pin_tier.ensure(16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+        HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(c->tier_ev, s));
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
@@ -1484,10 +1499,9 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
                                                 c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                                 c->bucket_unique.as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
                                                 s));
-        uint32_t ntier[2] = {0, 0};
-        HIP_TRY(hipMemcpyAsync(ntier, c->misc.p, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-    htrace("sorted: tiers read");
+        HIP_TRY(hipEventSynchronize(c->tier_ev));
+        uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
+        htrace("sorted: tiers read");
         if (ntier[0] && c->KW == 1)
             HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), ntier[0], k,
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
@@ -1555,20 +1569,44 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     }
     HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
-    uint64_t distinct = 0;
-    HIP_TRY(hipMemcpyAsync(&distinct, c->dense_off.as<uint64_t>() + nbuckets, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    htrace("sorted: distinct read");
-    FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
-    FK_TRY(ensure(c->dense_counts, distinct * 4));
+    // the dense result sized for every key (a bound on the distinct keys) when the device has room
+    // for it twice over: the compaction is then queued without waiting for the distinct total,
+    // which arrives with the bin offsets (resolve_distinct); else the total is read first
+    const uint64_t bound_keys = total_kmers * 8 * c->KW, bound_counts = total_kmers * 4;
+    bool bounded = c->dense_keys.bytes >= bound_keys && c->dense_counts.bytes >= bound_counts;
+    if (!bounded) {
+        size_t free_b = 0, total_b = 0;
+        const uint64_t grow = bound_keys + bound_counts - std::min<uint64_t>(c->dense_keys.bytes + c->dense_counts.bytes,
+                                                                               bound_keys + bound_counts);
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (uint64_t)free_b > 2 * grow) {
+            FK_TRY(ensure(c->dense_keys, bound_keys));
+            FK_TRY(ensure(c->dense_counts, bound_counts));
+            bounded = true;
+        }
+        (void)hipGetLastError();
+    }
+    if (!bounded) {
+        uint64_t distinct = 0;
+        HIP_TRY(hipMemcpyAsync(&distinct, c->dense_off.as<uint64_t>() + nbuckets, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        htrace("sorted: distinct read");
+        FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
+        FK_TRY(ensure(c->dense_counts, distinct * 4));
+    }
     FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
     HIP_TRY(launch_bucket_compact(c->KW, c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                   c->buckets.as<Bucket>(), nbuckets, c->dense_off.as<uint64_t>(),
                                   c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(), s));
     HIP_TRY(launch_bin_offsets(c->flag_scan.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
                                c->bin_off.as<uint64_t>(), s));
-    c->distinct = distinct;
+    c->distinct_pending = true;
     return FK_OK;
+}
+
+// After the bin offsets are on the host: the sorted count's distinct total is their last entry.
+static void resolve_distinct(fk_ctx *c) {
+    if (c->distinct_pending && !c->h_bin_off.empty()) c->distinct = c->h_bin_off.back();
+    c->distinct_pending = false;
 }
 
 static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint64_t max_bin_kmers) {
@@ -1810,6 +1848,7 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
     HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memcpy(c->h_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
+    resolve_distinct(c);
     htrace("tail: bin offsets read");
     c->stats.records_received = nrecv;
     c->stats.distinct = c->distinct;
@@ -2201,6 +2240,7 @@ static int staged_count(fk_ctx *c) {
     HIP_TRY(hipMemcpyAsync(c->pin_down.p, c->bin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memcpy(c->h_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
+    resolve_distinct(c);
     htrace("staged: bin offsets read");
     double mp = 0.0, mx = 0.0;
     for (uint32_t p = 0; p < c->st_np; ++p) {
