@@ -73,6 +73,18 @@ def test_piece_counts_disjoint_and_skewed_pieces(small_pieces):
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
 
 
+def test_piece_counts_piece_without_kmers(small_pieces):
+    # pieces that hold no k-mer at all (reads of N only) between pieces that do: the staged path
+    # skips them (no key array, no piece), the merge path counts them as empty
+    a = fk.synth_fasta(8_000, 100, 300_000, seed=0xA7)
+    nn = b"".join(b">n%d\n" % i + b"N" * 100 + b"\n" for i in range(20_000))
+    b = fk.synth_fasta(8_000, 100, 300_000, seed=0xA8, first_read=8_000)
+    fasta = a + nn + b
+    kc = count_pinned(fasta, 28, 10)
+    assert kc.stats()["pieces_counted"] >= 2
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
+
+
 def test_piece_counts_long_sequence(small_pieces):
     rng = np.random.default_rng(5)
     seq = np.frombuffer(b"ACGTN", dtype=np.uint8)[rng.choice(5, 3_000_000, p=[.245, .245, .245, .245, .02])]
