@@ -281,6 +281,12 @@ def main() -> None:
 
     # leg 1 (SURVEY 8d's timer, the headline): FASTA in pinned host memory -> counts on the device
     elapsed, host_stats = timed("step_host", args.steps, args.warmup)
+    if os.environ.get("FASTKMER_BENCH_MEMINFO"):  # device memory left after the host-input leg
+        free_b, total_b = torch.cuda.mem_get_info()
+        st0 = host_stats[-1][0]
+        print(f"meminfo: {free_b / 1e9:.1f} GB free of {total_b / 1e9:.1f} GB after the host-input leg; "
+              f"buckets {st0['buckets']}, oversize {st0['oversize_buckets']}, fine bits {st0['fine_bits']}",
+              file=sys.stderr, flush=True)
     host_sizes = [r.kc.bin_sizes() for r in ranks]
     for r, s in zip(ranks, host_sizes):
         assert int(s.sum()) == host_stats[-1][ranks.index(r)]["distinct"] > 0

@@ -371,7 +371,7 @@ struct fk_ctx {
     uint32_t st_np = 0;                          // pieces expanded in the current job
     SortedPlan st_plan;                          // the job's cells (fixed by its first piece)
     uint64_t st_kmers = 0;                       // k-mers expanded so far
-    DevBuf st_keys[STAGE_MAXP], st_cb[STAGE_MAXP], st_total, gathered, piece_starts;
+    DevBuf st_keys[STAGE_MAXP], st_cb[STAGE_MAXP], st_total, piece_starts;
     int st_starts = 1;                           // FASTKMER_STAGED_STARTS=0: the wave tier reads st_cb itself
     hipEvent_t st_ev[4 * STAGE_MAXP] = {};       // per piece: partition begin / end, expansion begin / end
 
@@ -675,7 +675,6 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
         if (ev) (void)hipEventDestroy(ev);
     for (int p = 0; p < STAGE_MAXP; ++p) release(c->st_keys[p]), release(c->st_cb[p]);
     release(c->st_total);
-    release(c->gathered);
     release(c->piece_starts);
     if (c->seg_ev) (void)hipEventDestroy(c->seg_ev);
     for (auto &ev : c->h2d_ev)
@@ -1441,9 +1440,6 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     FK_TRY(ensure(c->flags, ncell_all * 4));
     FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
-    // the streaming radix path reads one contiguous array: the staged pieces' large buckets are
-    // gathered into c->gathered first
-    const uint64_t *flat_keys = src_in.keys;
     // 4c: buckets.  Tiered (k <= 32): cells packed greedily into buckets of
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
@@ -1507,18 +1503,11 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
                                           c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
                                           cap, 99, lists, s));
-        else if (ntier[0]) {
-            if (src.np > 0) {  // the 128-bit block tier reads one contiguous array
-                FK_TRY(ensure(c->gathered, total_kmers * 8 * c->KW));
-                HIP_TRY(launch_bucket_gather(c->KW, src, c->buckets.as<Bucket>(), lists, ntier[0],
-                                             c->gathered.as<uint64_t>(), s));
-                flat_keys = c->gathered.as<uint64_t>();
-            }
-            HIP_TRY(launch_bucket_sort(2, flat_keys, c->buckets.as<Bucket>(), ntier[0], k,
+        else if (ntier[0])
+            HIP_TRY(launch_bucket_sort(2, src, c->buckets.as<Bucket>(), ntier[0], k,
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, s));
-        }
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
             // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
@@ -1531,13 +1520,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         }
         if (nlarge) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            if (src.np > 0) {
-                FK_TRY(ensure(c->gathered, total_kmers * 8 * c->KW));
-                HIP_TRY(launch_bucket_gather(c->KW, src, c->buckets.as<Bucket>(), lists + nbuckets, ntier[1],
-                                             c->gathered.as<uint64_t>(), s));
-                flat_keys = c->gathered.as<uint64_t>();
-            }
-            HIP_TRY(launch_bucket_sort_large(c->KW, flat_keys, c->buckets.as<Bucket>(), ntier[1], k,
+            HIP_TRY(launch_bucket_sort_large(c->KW, src, c->buckets.as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              lists + nbuckets, s));
@@ -1551,7 +1534,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
                                           small_limit, c->dbg_phase, nullptr, s));
         else
-            HIP_TRY(launch_bucket_sort(c->KW, src.keys, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_sort(c->KW, src, c->buckets.as<Bucket>(), nbuckets, k,
                                        c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
                                        small_limit, nullptr, s));
@@ -1561,7 +1544,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         c->stats.oversize_buckets = oversize;
         if (oversize) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            HIP_TRY(launch_bucket_sort_large(c->KW, src.keys, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_sort_large(c->KW, src, c->buckets.as<Bucket>(), nbuckets, k,
                                              c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              nullptr, s));
@@ -1569,8 +1552,8 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     }
     HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
-    // the dense result sized for every key (a bound on the distinct keys) when the device has room
-    // for it twice over: the compaction is then queued without waiting for the distinct total,
+    // the dense result sized for every key (a bound on the distinct keys) when that is at most a
+    // tenth of the device and fits twice over in its free memory: the compaction is then queued without waiting for the distinct total,
     // which arrives with the bin offsets (resolve_distinct); else the total is read first
     const uint64_t bound_keys = total_kmers * 8 * c->KW, bound_counts = total_kmers * 4;
     bool bounded = c->dense_keys.bytes >= bound_keys && c->dense_counts.bytes >= bound_counts;
@@ -1578,7 +1561,8 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         size_t free_b = 0, total_b = 0;
         const uint64_t grow = bound_keys + bound_counts - std::min<uint64_t>(c->dense_keys.bytes + c->dense_counts.bytes,
                                                                                bound_keys + bound_counts);
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (uint64_t)free_b > 2 * grow) {
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (uint64_t)free_b > 2 * grow &&
+            grow <= (uint64_t)total_b / 10) {
             FK_TRY(ensure(c->dense_keys, bound_keys));
             FK_TRY(ensure(c->dense_counts, bound_counts));
             bounded = true;

@@ -215,17 +215,14 @@ hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *bucket
                                       uint32_t wave_cap, uint32_t wave_slots, const uint32_t *list, hipStream_t s);
 // staged pieces (src.np > 0) in the wave tier: the default tier configuration only
 bool wave_staged_supported(uint32_t wave_cap, uint32_t wave_slots, int bpw);
-// keys of the listed buckets from the staged pieces to out[begin, begin + n)
-hipError_t launch_bucket_gather(int KW, const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
-                                uint64_t nlist, uint64_t *out, hipStream_t s);
 // staged pieces in the 128-bit wave tier: the default table size only
 bool wave128_staged_supported(uint32_t wave_slots);
 // dst[i] += src[i] (dst = src when `copy`)
 hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
-hipError_t launch_bucket_sort(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
+hipError_t launch_bucket_sort(int KW, const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                               unsigned long long *oversize, uint32_t small_limit, const uint32_t *list, hipStream_t s);
-hipError_t launch_bucket_sort_large(int KW, const uint64_t *keys, const Bucket *buckets, uint64_t nbuckets, int k,
+hipError_t launch_bucket_sort_large(int KW, const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                     uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
                                     uint64_t *bucket_unique, const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_t *out_counts,
