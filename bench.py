@@ -23,9 +23,9 @@ fused kernel mapping every landed tile meanwhile, and with N > 1 every landed
 piece exchanged while the next one is copied) and ends with the counts on the
 device.  `device_resident_value` is the same job with the FASTA already in HBM;
 the roofline of the fused encode+signature kernel comes from that leg (HIP
-events around its one launch, on the stream it runs on).  With N > 1 that leg
-runs only with --device-leg (a rank's 6.25 GB shard would otherwise hold both
-legs' buffers on its GPU at once).
+events around its one launch, on the stream it runs on).  With N > 1, or more
+than 2 GB per GPU, that leg runs only with --device-leg (a rank's 6.25 GB shard
+would otherwise hold both legs' buffers on its GPU at once).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         (N > 1: torchrun --nproc-per-node N bench.py --gpus N ...; one process per GPU,
@@ -197,8 +197,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-device-leg", action="store_true", help="skip the HBM-resident leg (no roofline)")
     ap.add_argument("--device-leg", action="store_true",
-                    help="run the HBM-resident leg with N > 1 too (default: N = 1 only; at N > 1 each rank's "
-                         "6.25 GB shard would hold both legs' buffers on its GPU at once)")
+                    help="run the HBM-resident leg with N > 1 or > 2 GB per GPU too (default: N = 1 at <= 2 GB "
+                         "only; a 6.25 GB shard would hold both legs' buffers on its GPU at once)")
     ap.add_argument("--use-ht", action="store_true", help="hash count (extractKXmersHT, useHT=1)")
     ap.add_argument("--workload", default="", choices=["", "c2", "c3", "c4", "c5"],
                     help="c2 = BASELINE configs[1] (default at N = 1); c3 = configs[2] (default at N > 1); "
@@ -216,10 +216,12 @@ def main() -> None:
         raise SystemExit("--rehearse-local runs in one process")
     n_ranks = local or world
     wl = args.workload or ("c2" if n_ranks == 1 else "c3")
-    if n_ranks > 1 and not args.device_leg:
-        args.no_device_leg = True  # the roofline leg is the N = 1 line's
     if not args.bytes_per_gpu:
         args.bytes_per_gpu = WORKLOADS[wl][6]
+    # the roofline leg is the N = 1 line's, at its 1 GB; a 6.25 GB shard (configs[2] / [3] per GPU)
+    # would hold both legs' buffers on its GPU at once (k = 55: ~57 GB per k-mer array)
+    if (n_ranks > 1 or args.bytes_per_gpu > 2_000_000_000) and not args.device_leg:
+        args.no_device_leg = True
     distributed = world > 1
     torch.cuda.set_device(0 if local else local_rank)
     if distributed:

@@ -254,6 +254,7 @@ struct fk_ctx {
     int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
     int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
+    int x2_l2 = 0;             // FASTKMER_X2_L2: level-2 workgroup size (128, 256, 512; 0 = by keys per super-cell)
     uint32_t greedy_cap = 0;   // FASTKMER_GREEDY_CAP (probe): pack cells into buckets of up to this many keys (0 = wave_cap)
     uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
     uint32_t wave_slots = 768;  // FASTKMER_WAVE_SLOTS: table slots of a 512-key wave bucket (768 or 1024;
@@ -367,7 +368,7 @@ struct fk_ctx {
     int piece_mode = 1;                          // FASTKMER_PIECE_MODE: 1 staged, 0 count + merge per piece
     std::vector<double> st_cuts{0.45, 0.7, 0.85};  // piece ends of a staged job (FASTKMER_PIECE_CUTS)
     bool st_cuts_set = false;
-    double st_one_level = 0.2;                   // FASTKMER_STAGED_ONE_LEVEL: one-pass expansion below this job fraction
+    double st_one_level = 0.0;                   // FASTKMER_STAGED_ONE_LEVEL: one-pass expansion below this job fraction
     uint32_t st_np = 0;                          // pieces expanded in the current job
     SortedPlan st_plan;                          // the job's cells (fixed by its first piece)
     uint64_t st_kmers = 0;                       // k-mers expanded so far
@@ -520,6 +521,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
     if (const char *x1 = getenv("FASTKMER_X2_L1"); x1 && x1[0]) c->x2_l1 = atoi(x1);
+    if (const char *x2 = getenv("FASTKMER_X2_L2"); x2 && x2[0]) c->x2_l2 = atoi(x2);
     const char *el = getenv("FASTKMER_EXPAND_LEVELS");
     if (el && el[0]) c->expand_levels = atoi(el);
     const char *wc = getenv("FASTKMER_WAVE_CAP");
@@ -1419,7 +1421,7 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
         FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
         HIP_TRY(launch_expand_two_level(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
                                         F2, c->lp.as<uint32_t>(), cell_base, c->mid.as<uint64_t>(),
-                                        keys.as<uint64_t>(), s, c->x2_l1));
+                                        keys.as<uint64_t>(), s, c->x2_l1, total_kmers, c->x2_l2));
     } else {
         HIP_TRY(launch_expand_scatter(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,
                                       c->lp.as<uint32_t>(), cell_base, keys.as<uint64_t>(),
@@ -2170,8 +2172,9 @@ static int staged_expand_chunks(fk_ctx *c, uint32_t nchunks, const std::vector<u
         if (!c->st_plan.tiered || !c->st_plan.two_level)
             return set_err(FK_E_STATE, "staged pieces need the tiered two-level count");
     }
-    // a small piece (FASTKMER_STAGED_ONE_LEVEL: below this fraction of the job) is scattered to its
-    // cells in one pass: the second pass's cost per super-cell does not shrink with the piece
+    // a small piece (FASTKMER_STAGED_ONE_LEVEL: below this fraction of the job; default none) is
+    // scattered to its cells in one pass.  Off since level 2 sizes its workgroups to the keys per
+    // super-cell (a 15 % piece: 1.14 ms one-pass against ~0.75 ms for both levels).
     SortedPlan pl = c->st_plan;
     if (frac > 0.0 && frac < c->st_one_level && pl.F <= MAX_FINE_BITS - 1) pl.two_level = false;
     HIP_TRY(hipEventRecord(c->st_ev[4 * p + 2], s));

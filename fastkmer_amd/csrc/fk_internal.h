@@ -194,7 +194,7 @@ hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *bucke
 hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
                                    uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
                                    const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s,
-                                   int l1_threads = 0);
+                                   int l1_threads = 0, uint64_t nkeys = 0, int l2_threads = 0);
 hipError_t launch_expand_hist_sc(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
                                  int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);
 // pieces of bins (x = local bin, y / z = chunk range, w = whole bin): the same per piece, then the
