@@ -1871,6 +1871,12 @@ static int partition_src(fk_ctx *c, const RecSrc &src, uint64_t &nrecv, std::vec
     HIP_TRY(hipEventRecord(e0, s));
     FK_TRY(part_count(c->part, src, 1, c->G, local_table(c), nlb, c->ws, s));
     htrace("reduce_src: part_count queued");
+    // the scatter needs only the device-side offsets: it is queued before the host reads the part
+    // totals (the output sized for src.nrec, for tiled sources the slot count: an upper bound), so
+    // the GPU scatters while the host builds and uploads the chunk table
+    FK_TRY(ensure(c->precs, src.nrec * c->W * 8));
+    FK_TRY(part_scatter(c->part, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
+    htrace("reduce_src: scatter queued");
     std::vector<uint64_t> brec(nlb);
     bkm.assign(nlb, 0);
     if (c->pin_down.ensure((size_t)nlb * 16 + 16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
@@ -1896,11 +1902,8 @@ static int partition_src(fk_ctx *c, const RecSrc &src, uint64_t &nrecv, std::vec
         return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
                        (unsigned long long)off, (unsigned long long)nrecv);
     build_chunks(nlb, ranges, chunks, bcb);
-    FK_TRY(ensure(c->precs, nrecv * c->W * 8));
     FK_TRY(upload_chunks(c, chunks, bcb));
     htrace("reduce_src: chunks uploaded");
-    FK_TRY(part_scatter(c->part, 1, c->G, local_table(c), c->precs.as<uint64_t>(), s));
-    htrace("reduce_src: scatter queued");
     HIP_TRY(hipEventRecord(e1, s));
     c->rsrc = c->precs.as<uint64_t>();
     return FK_OK;
