@@ -1890,18 +1890,29 @@ static int partition_src(fk_ctx *c, const RecSrc &src, uint64_t &nrecv, std::vec
         memcpy(bkm.data(), c->pin_down.as<uint64_t>() + nlb, nlb * 8);
     }
     htrace("reduce_src: part counts read");
-    // record offsets per local bin after the partition
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges(nlb);
-    uint64_t off = 0;
+    // the bins' records are consecutive after the partition: chunks straight from the bin totals (no
+    // per-bin range lists: the host is on the critical path between the read-back and the upload)
+    uint64_t off = 0, nch = 0;
     for (uint32_t lb = 0; lb < nlb; ++lb) {
-        ranges[lb].push_back({off, off + brec[lb]});
         off += brec[lb];
+        nch += (brec[lb] + CHUNK_RECORDS - 1) / CHUNK_RECORDS;
     }
     if (src.tcnt) nrecv = off;
     if (off != nrecv)
         return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
                        (unsigned long long)off, (unsigned long long)nrecv);
-    build_chunks(nlb, ranges, chunks, bcb);
+    chunks.resize(nch);
+    bcb.assign((size_t)nlb + 1, 0);
+    off = 0;
+    uint32_t ci = 0;
+    for (uint32_t lb = 0; lb < nlb; ++lb) {
+        bcb[lb] = ci;
+        const uint64_t end = off + brec[lb];
+        for (uint64_t r = off; r < end; r += CHUNK_RECORDS)
+            chunks[ci++] = Chunk{r, std::min<uint64_t>(r + CHUNK_RECORDS, end), lb, 0u};
+        off = end;
+    }
+    bcb[nlb] = ci;
     FK_TRY(upload_chunks(c, chunks, bcb));
     htrace("reduce_src: chunks uploaded");
     HIP_TRY(hipEventRecord(e1, s));
