@@ -107,6 +107,8 @@ def lib():
         "fk_ingest": (ctypes.c_int, [P, ctypes.c_char_p, SZ, ctypes.c_int]),
         "fk_ingest_device": (ctypes.c_int, [P, P, SZ, ctypes.c_int]),
         "fk_ingest_reserve": (ctypes.c_int, [P, U64]),
+        "fk_split_bytes": (ctypes.c_int, [ctypes.c_char_p, I32, I32, I32, I32, P, SZ, ctypes.POINTER(SZ)]),
+        "fk_ingest_file_range": (ctypes.c_int, [P, ctypes.c_char_p, I32, I32, U64]),
         "fk_synth_fasta_device": (ctypes.c_int, [P, U64, U64, I32, U64, U64, ctypes.c_double, ctypes.c_double]),
         "fk_synth_fasta_to_device": (ctypes.c_int, [P, U64, U64, I32, U64, U64, ctypes.c_double, ctypes.c_double]),
         "fk_map": (ctypes.c_int, [P, P]),
@@ -193,6 +195,18 @@ def synth_fasta_to_device(ptr: int, n_reads: int, read_len: int = 100, genome_le
     _check(L.fk_synth_fasta_to_device(ctypes.c_void_p(ptr), first_read, n_reads, read_len, genome_len, seed,
                                       err_rate, n_rate))
     return n_reads * L.fk_synth_record_bytes(read_len)
+
+
+def split_bytes(path: str, world: int, rank: int, k: int, sequence_type: int = 0) -> bytes:
+    """The bytes rank `rank` of `world` ingests from the FASTA file at `path` (fk_split_bytes: the
+    FASTdoop-style input split of SBKC:993, 1009-1012; host only)."""
+    L = lib()
+    n = ctypes.c_size_t()
+    p = os.fsencode(path)
+    _check(L.fk_split_bytes(p, world, rank, k, sequence_type, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(max(n.value, 1))
+    _check(L.fk_split_bytes(p, world, rank, k, sequence_type, buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value]
 
 
 def decode_keys(keys: np.ndarray, k: int) -> list[str]:
@@ -292,6 +306,13 @@ class KmerCounter:
     def reserve(self, total_bytes: int) -> None:
         """Size the device input for a streamed ingest of about total_bytes."""
         _check(lib().fk_ingest_reserve(self._h, total_bytes))
+
+    def ingest_file_range(self, path: str, world: int | None = None, rank: int | None = None,
+                          window_bytes: int = 0) -> None:
+        """The job's input from a file: this rank's split (fk_ingest_file_range; world / rank
+        default to the context's), read in pinned windows while earlier ones are copied and mapped."""
+        _check(lib().fk_ingest_file_range(self._h, os.fsencode(path), self.n_ranks if world is None else world,
+                                          self.rank if rank is None else rank, window_bytes))
 
     def ingest_device(self, ptr: int, n: int) -> None:
         _check(lib().fk_ingest_device(self._h, ctypes.c_void_p(ptr), n, 1))

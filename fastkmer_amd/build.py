@@ -20,8 +20,8 @@ CLI = os.path.join(PKG, "bin", "fastkmer-cli")
 ARCH = os.environ.get("FASTKMER_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-LIB_SOURCES = ["fk_kernels.hip", "fk_api.cpp", "fk_comm.cpp"]
-DEPS = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".inc", ".h")) or f in ("fk_api.cpp", "fk_comm.cpp"))
+LIB_SOURCES = ["fk_kernels.hip", "fk_api.cpp", "fk_comm.cpp", "fk_split.cpp"]
+DEPS = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".inc", ".h")) or f in ("fk_api.cpp", "fk_comm.cpp", "fk_split.cpp"))
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -58,12 +58,12 @@ def _resource_table(remarks: str) -> list[dict]:
     return rows
 
 
-def _compile_kernels(src: str, obj: str) -> None:
+def _compile_kernels(src: str, obj: str, defs: list[str] = ()) -> None:
     """Compile the kernel file with resource-usage remarks; no kernel may use
     scratch (a spilled register array costs a global-memory round trip per
     access, e.g. 1.57 -> 2.38 ms for the signature kernel)."""
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
-           "-Wno-unused-function", "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", obj]
+           "-Wno-unused-function", *defs, "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", obj]
     print("+", " ".join(cmd), flush=True)
     r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
     rows = _resource_table(r.stderr)
@@ -73,33 +73,52 @@ def _compile_kernels(src: str, obj: str) -> None:
         print(other, file=sys.stderr)
     if r.returncode != 0:
         raise subprocess.CalledProcessError(r.returncode, cmd)
-    with open(RESOURCES, "w") as f:
+    resources = os.path.join(os.path.dirname(obj), "kernel_resources.txt")
+    with open(resources, "w") as f:
         f.write("kernel\tVGPRs\tAGPRs\tscratch_B_per_lane\toccupancy_waves_per_SIMD\tLDS_B\n")
         for row in rows:
             f.write("\t".join(str(row.get(c, "")) for c in
                                ("kernel", "VGPRs", "AGPRs", "ScratchSize", "Occupancy", "LDS")) + "\n")
     bad = [row["kernel"] for row in rows if row.get("ScratchSize", 0) or row.get("VGPRs Spill", 0)]
     if bad:
-        raise RuntimeError(f"kernels using scratch memory (see {RESOURCES}): {bad}")
+        raise RuntimeError(f"kernels using scratch memory (see {resources}): {bad}")
+
+
+PROBES_LIB = os.path.join(PKG, "lib_probes", "libfastkmer.so")
+
+
+def _build_lib(lib: str, deps: list[str], force: bool, defs: list[str]) -> None:
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if not (force or _stale(lib, deps)):
+        return
+    objs = []
+    for src in LIB_SOURCES:
+        obj = os.path.join(os.path.dirname(lib), os.path.splitext(src)[0] + ".o")
+        if src.endswith(".hip"):
+            _compile_kernels(os.path.join(CSRC, src), obj, defs)
+        else:
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+                  "-Wall", "-Wno-unused-function", *defs, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-ldl"])
+    for o in objs:
+        os.remove(o)
+
+
+def build_probes(force: bool = False) -> str:
+    """A measurement-only library with the result-altering timing probes compiled in (-DFK_PROBES:
+    FASTKMER_FUSED_PROBE, FASTKMER_DEBUG_PHASE, FASTKMER_LH_PROBE, FASTKMER_DEBUG_SCATTER=2/3).
+    Scripts select it with FASTKMER_LIB; nothing else loads it."""
+    deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "fastkmer.h")]
+    _build_lib(PROBES_LIB, deps, force, ["-DFK_PROBES"])
+    return PROBES_LIB
 
 
 def build(force: bool = False) -> str:
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     os.makedirs(os.path.dirname(CLI), exist_ok=True)
     deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "fastkmer.h")]
-    if force or _stale(LIB, deps):
-        objs = []
-        for src in LIB_SOURCES:
-            obj = os.path.join(PKG, "lib", os.path.splitext(src)[0] + ".o")
-            if src.endswith(".hip"):
-                _compile_kernels(os.path.join(CSRC, src), obj)
-            else:
-                _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
-                      "-Wall", "-Wno-unused-function", "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj])
-            objs.append(obj)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-ldl"])
-        for o in objs:
-            os.remove(o)
+    _build_lib(LIB, deps, force, [])
     if force or _stale(CLI, [os.path.join(CSRC, "fk_cli.cpp"), LIB]):
         _run(["g++", "-O2", "-std=c++17", "-o", CLI, os.path.join(CSRC, "fk_cli.cpp"),
               f"-L{os.path.dirname(LIB)}", "-lfastkmer", "-Wl,-rpath,$ORIGIN/../lib"])
@@ -136,4 +155,7 @@ def build_jni(force: bool = False) -> str | None:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--probes" in sys.argv:
+        build_probes(force="--force" in sys.argv)
+    else:
+        build(force="--force" in sys.argv)

@@ -5,7 +5,9 @@
 // the map closure, the reduceByKey shuffle and the reduce closure.  All device
 // memory is owned by the context and reused across calls (grow-only).
 #include <errno.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -22,6 +24,7 @@
 #include "../../include/fastkmer.h"
 #include "fk_comm.h"
 #include "fk_internal.h"
+#include "fk_split.h"
 
 #define FK_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -335,6 +338,7 @@ struct fk_ctx {
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
     PinBuf pin_up, pin_down, pin_merge;  // staging: chunk tables up, per-bin counts down, merge tables up
     PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
+    PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
     bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
 
@@ -516,10 +520,17 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->force_large = dbg && dbg[0] == '1';
     const char *ct = getenv("FASTKMER_DEBUG_CELL_TARGET");
     c->cell_target = ct ? (uint32_t)atoi(ct) : 0u;
+    // Result-altering timing probes (a kernel stopped after a phase, a scatter that drops keys)
+    // exist only in a library built with -DFK_PROBES (python -m fastkmer_amd.build --probes); the
+    // product library reads none of them.  FASTKMER_DEBUG_SCATTER=0 (the plain scatter, exact)
+    // stays available everywhere.
     const char *sc = getenv("FASTKMER_DEBUG_SCATTER");
-    c->scatter_wc = (sc && sc[0]) ? atoi(sc) : 1;
+    if (sc && sc[0] && atoi(sc) == 0) c->scatter_wc = 0;
+#ifdef FK_PROBES
+    if (sc && sc[0]) c->scatter_wc = atoi(sc);
     const char *ph = getenv("FASTKMER_DEBUG_PHASE");
     if (ph && ph[0]) c->dbg_phase = atoi(ph);
+#endif
     if (const char *x1 = getenv("FASTKMER_X2_L1"); x1 && x1[0]) c->x2_l1 = atoi(x1);
     if (const char *x2 = getenv("FASTKMER_X2_L2"); x2 && x2[0]) c->x2_l2 = atoi(x2);
     const char *el = getenv("FASTKMER_EXPAND_LEVELS");
@@ -539,12 +550,14 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (fu && fu[0]) c->fused = atoi(fu);
     const char *fn = getenv("FASTKMER_FUSED_NT");
     if (fn && fn[0]) c->fused_nt = atoi(fn) == 256 ? 256 : 512;
+#ifdef FK_PROBES
     const char *fp = getenv("FASTKMER_FUSED_PROBE");
     if (fp && fp[0]) c->fused_probe = atoi(fp);
-    const char *lh = getenv("FASTKMER_LDS_HT");
-    if (lh && lh[0]) c->lh_mode = atoi(lh);
     const char *lp = getenv("FASTKMER_LH_PROBE");
     if (lp && lp[0]) c->lh_probe = atoi(lp);
+#endif
+    const char *lh = getenv("FASTKMER_LDS_HT");
+    if (lh && lh[0]) c->lh_mode = atoi(lh);
     if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
         c->piece_bytes_set = true;
@@ -651,6 +664,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->pin_down.release();
     c->pin_merge.release();
     c->pin_tier.release();
+    c->file_pin[0].release();
+    c->file_pin[1].release();
     if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
     release(c->xsend);
     release(c->xrecv);
@@ -771,8 +786,10 @@ static void pieces_reset(fk_ctx *c);
 // so the PCIe transfer hides the parse + signature work.  Returns once the
 // source has been read (the caller's buffer is free); the map of the last
 // segment may still be running.
-FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
-    if (!c || (!fasta && n)) return set_err(FK_E_INVALID, "null argument");
+static int comm_fail(fk_ctx *c, int rc);
+
+static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
+    if (!fasta && n) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
     if (c->d_fasta && c->d_fasta != c->fasta_own.as<uint8_t>()) {
         // a borrowed device input (fk_ingest_device): host chunks cannot be appended
@@ -894,8 +911,22 @@ FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     return FK_OK;
 }
 
+// fk_ingest is collective with a communicator (pieces are exchanged while the input lands): any
+// error on this rank aborts the group, so peers blocked in a step return instead of waiting.
+FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    const int rc = ingest_impl(c, fasta, n, last);
+    return rc && c->comm ? comm_fail(c, rc) : rc;
+}
+
+static int reserve_impl(fk_ctx *c, uint64_t total_bytes);
+
 FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
+    return reserve_impl(c, total_bytes);
+}
+
+static int reserve_impl(fk_ctx *c, uint64_t total_bytes) {
     DeviceGuard dg_(c->device);
     if (!c->ingest_fresh && c->d_fasta) return set_err(FK_E_STATE, "fk_ingest_reserve inside a streamed input");
     FK_TRY(ensure(c->fasta_own, total_bytes));
@@ -911,8 +942,99 @@ FK_EXPORT int fk_ingest_reserve(fk_ctx *c, uint64_t total_bytes) {
     return FK_OK;
 }
 
+// ---- a rank's split of a FASTA file (fk_split.cpp)
+
+namespace {
+struct Fd {
+    int fd = -1;
+    ~Fd() {
+        if (fd >= 0) close(fd);
+    }
+};
+int open_split(const char *path, int32_t world, int32_t rank, int32_t k, int32_t seq, Fd &f, uint64_t &size,
+               SplitPlan &plan) {
+    f.fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (f.fd < 0) return set_err(FK_E_IO, "open(%s): %s", path, strerror(errno));
+    struct stat st {};
+    if (fstat(f.fd, &st) != 0) return set_err(FK_E_IO, "fstat(%s): %s", path, strerror(errno));
+    size = (uint64_t)st.st_size;
+    std::string err;
+    if (seq != 0 && seq != 1) return set_err(FK_E_INVALID, "sequence_type must be 0 or 1");
+    if (plan_split(f.fd, size, world, rank, k, seq, plan, err))
+        return set_err(world < 1 || rank < 0 || rank >= world || k < 1 ? FK_E_INVALID : FK_E_IO, "%s: %s", path,
+                       err.c_str());
+    return FK_OK;
+}
+}  // namespace
+
+FK_EXPORT int fk_split_bytes(const char *path, int32_t world, int32_t rank, int32_t k, int32_t sequence_type,
+                             uint8_t *out, size_t cap, size_t *n) {
+    if (!path || !n) return set_err(FK_E_INVALID, "null argument");
+    Fd f;
+    uint64_t size = 0;
+    SplitPlan plan;
+    FK_TRY(open_split(path, world, rank, k, sequence_type, f, size, plan));
+    *n = (size_t)plan.total;
+    if (!out) return FK_OK;
+    if (cap < plan.total) return set_err(FK_E_RANGE, "split of %llu bytes, buffer holds %zu", (unsigned long long)plan.total, cap);
+    std::string err;
+    if (read_split(f.fd, size, plan, 0, plan.total, out, err)) return set_err(FK_E_IO, "%s: %s", path, err.c_str());
+    return FK_OK;
+}
+
+static int ingest_file_impl(fk_ctx *c, const char *path, int32_t world, int32_t rank, uint64_t window) {
+    if (!path) return set_err(FK_E_INVALID, "null path");
+    if (!c->ingest_fresh && c->d_fasta) return set_err(FK_E_STATE, "fk_ingest_file_range inside a streamed input");
+    Fd f;
+    uint64_t size = 0;
+    SplitPlan plan;
+    FK_TRY(open_split(path, world, rank, c->cfg.k, c->cfg.sequence_type, f, size, plan));
+    const uint64_t total = plan.total;
+    if (total == 0) return ingest_impl(c, nullptr, 0, 1);
+    if (!window) window = 256ull << 20;
+    window = std::max<uint64_t>(window, 1ull << 20);
+    const uint64_t win = std::min(window, total);
+    for (int i = 0; i < 2 && i * win < total; ++i)
+        if (c->file_pin[i].ensure(win)) return set_err(FK_E_NOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)win);
+    FK_TRY(reserve_impl(c, total));
+    std::string rerr;
+    int rrc = read_split(f.fd, size, plan, 0, win, c->file_pin[0].as<uint8_t>(), rerr);
+    if (rrc) return set_err(FK_E_IO, "%s: %s", path, rerr.c_str());
+    int b = 0;
+    for (uint64_t pos = 0; pos < total;) {
+        const uint64_t len = std::min(win, total - pos), next = std::min(win, total - pos - len);
+        // the next window is read while this one is copied and mapped
+        std::thread reader;
+        if (next)
+            reader = std::thread([&, b, pos, len, next] {
+                rrc = read_split(f.fd, size, plan, pos + len, next, c->file_pin[b ^ 1].as<uint8_t>(), rerr);
+            });
+        const int rc = ingest_impl(c, c->file_pin[b].as<uint8_t>(), len, pos + len == total ? 1 : 0);
+        if (reader.joinable()) reader.join();
+        if (rc) return rc;
+        if (rrc) return set_err(FK_E_IO, "%s: %s", path, rerr.c_str());
+        pos += len;
+        b ^= 1;
+    }
+    return FK_OK;
+}
+
+FK_EXPORT int fk_ingest_file_range(fk_ctx *c, const char *path, int32_t world, int32_t rank, uint64_t window_bytes) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    const int rc = ingest_file_impl(c, path, world, rank, window_bytes);
+    return rc && c->comm ? comm_fail(c, rc) : rc;
+}
+
+static int ingest_device_impl(fk_ctx *c, const void *d, size_t n, int last);
+
 FK_EXPORT int fk_ingest_device(fk_ctx *c, const void *d, size_t n, int last) {
-    if (!c || (!d && n)) return set_err(FK_E_INVALID, "null argument");
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    const int rc = ingest_device_impl(c, d, n, last);
+    return rc && c->comm ? comm_fail(c, rc) : rc;
+}
+
+static int ingest_device_impl(fk_ctx *c, const void *d, size_t n, int last) {
+    if (!d && n) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
     if (c->comm && c->xch.open) return set_err(FK_E_STATE, "fk_ingest_device: the previous job's exchange is unfinished");
     if (c->comm) xch_reset(c);
@@ -1897,7 +2019,12 @@ static int partition_src(fk_ctx *c, const RecSrc &src, uint64_t &nrecv, std::vec
         off += brec[lb];
         nch += (brec[lb] + CHUNK_RECORDS - 1) / CHUNK_RECORDS;
     }
-    if (src.tcnt) nrecv = off;
+    if (src.tcnt) {
+        // a tiled source (the fused map's slots) holds this rank's own input, all of it owned only
+        // with one rank; its record total is the partition's
+        if (c->G != 1) return set_err(FK_E_STATE, "tiled records partitioned on a context of %u ranks", c->G);
+        nrecv = off;
+    }
     if (off != nrecv)
         return set_err(FK_E_INVALID, "received records belong to bins of another rank (%llu of %llu owned)",
                        (unsigned long long)off, (unsigned long long)nrecv);
@@ -2029,7 +2156,12 @@ static void pieces_reset(fk_ctx *c) {
 
 // Pieces are counted separately for the sorted count (its results merge in key order); the hash
 // count's table order does not, it counts the whole input at the end.
-static bool piece_counting(const fk_ctx *c) { return c->count_pieces && !c->pieces_void && !c->cfg.use_ht; }
+// One rank counts pieces of its own input only without a communicator and with G == 1 (a context
+// of G > 1 ranks without one maps for a caller-driven exchange, fk_map_emit: its input holds
+// other ranks' records); with a communicator the received segments are the pieces.
+static bool piece_counting(const fk_ctx *c) {
+    return c->count_pieces && !c->pieces_void && !c->cfg.use_ht && (c->comm || c->G == 1);
+}
 
 static void swap_result(fk_ctx *c, fk_ctx::PieceRes &r) {
     std::swap(r.keys, c->dense_keys);
@@ -2660,7 +2792,8 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     if (c->comm) {
         DeviceGuard dg_(c->device);
-        return finish_exchange(c);
+        const int rc = finish_exchange(c);
+        return rc ? comm_fail(c, rc) : rc;  // collective: a failed rank fails the group
     }
     if (c->G != 1)
         return set_err(FK_E_STATE, "fk_finish over %u ranks needs a communicator (fk_comm_init); or use "

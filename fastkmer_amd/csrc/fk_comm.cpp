@@ -226,7 +226,9 @@ struct LocalGroup {
         } else {
             cv.wait(lk, [&] { return gen != g || failed; });
         }
-        if (failed) {
+        // a barrier every rank reached completed, whatever a rank did after leaving it (a rank
+        // destroyed right after the job's last barrier fails the group only for later collectives)
+        if (gen == g) {
             err = "a rank of the in-process group failed";
             return -1;
         }
@@ -246,6 +248,9 @@ class LocalComm : public Comm {
         rank_ = rank;
     }
     ~LocalComm() override {
+        // a rank that leaves fails the group: peers blocked in (or entering) a collective return
+        // an error instead of waiting for it
+        g_->fail();
         int prev = -1;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(dev_);

@@ -129,6 +129,28 @@ int fk_ingest(fk_ctx *ctx, const uint8_t *fasta, size_t n, int last);
  * fk_ingest call (a wrong size costs time, never results). */
 int fk_ingest_reserve(fk_ctx *ctx, uint64_t total_bytes);
 int fk_ingest_device(fk_ctx *ctx, const void *d_fasta, size_t n, int last);
+/* A rank's input split of a FASTA file, as the reference's FASTdoop input
+ * formats cut it for its map tasks (SBKC:993, 1009-1012): the file is cut into
+ * byte ranges of ~size/world.  sequence_type 0 (FASTAshortInputFileFormat):
+ * the whole records whose '>' lies in the rank's range.  sequence_type 1
+ * (FASTAlongInputFileFormat, overlap key "k"): the k-mer windows whose first
+ * base lies in the range -- a header line ">s\n", the range's bytes (after a
+ * header line it starts inside; nothing before the file's first header), the
+ * k - 1 sequence positions after it (stopping at a record boundary), "\n".
+ * The union of the ranks' counts is the whole file's.
+ *   fk_split_bytes: host only; the bytes rank `rank` ingests into out (cap
+ *     bytes; out = NULL: only *n, the split's size).
+ *   fk_ingest_file_range: the whole job input of this context from the file
+ *     (a fresh job, as one fk_ingest sequence with last = 1 at its end): the
+ *     split of (k, sequence_type) of the context's configuration, read with
+ *     positioned reads into two pinned windows of window_bytes (0: 256 MB;
+ *     the next window is read while the last one is copied and mapped), the
+ *     job's size announced first (fk_ingest_reserve).  Collective like
+ *     fk_ingest with a communicator.  world / rank: the split (usually the
+ *     context's n_ranks / rank). */
+int fk_split_bytes(const char *path, int32_t world, int32_t rank, int32_t k, int32_t sequence_type, uint8_t *out,
+                   size_t cap, size_t *n);
+int fk_ingest_file_range(fk_ctx *ctx, const char *path, int32_t world, int32_t rank, uint64_t window_bytes);
 /* Fill a caller's device buffer (current device) with the same bytes as
  * fk_synth_fasta_host (benchmarks: the input is staged to pinned host memory). */
 int fk_synth_fasta_to_device(void *d_out, uint64_t first_read, uint64_t n_reads, int32_t read_len,

@@ -277,3 +277,80 @@ def test_rccl_two_ranks_write_bins(tmp_path):
     assert sorted(os.listdir(out)) == files
     for f in files:
         assert (out / f).read_bytes() == (ref_dir / f).read_bytes(), f
+
+
+@pytest.mark.parametrize("how", ["bad_ingest", "destroyed"])
+def test_local_exchange_failing_rank_fails_the_group(small_pieces, how):
+    # an error on one rank of a collective entry point (fk_ingest / fk_finish with a
+    # communicator) aborts the group -- its peers return an error instead of blocking in a step.
+    # Rank 1 either fails its ingest (null source) or is destroyed without finishing.
+    fasta = fk.synth_fasta(20_000, 100, 400_000, seed=0xE8)
+    shards = record_shards(fasta, 2)
+    ctxs = [fk.KmerCounter(28, 10, 3, 2048, n_ranks=2, rank=r) for r in range(2)]
+    fk.comm_init_local(ctxs)
+    errs = [None, None]
+
+    def work(r):
+        try:
+            if r == 1:
+                if how == "bad_ingest":
+                    fk._check(fk.lib().fk_ingest(ctxs[1]._h, None, 100, 1))
+                else:
+                    ctxs[1].close()
+                return
+            ctxs[0].ingest(shards[0])
+            ctxs[0].finish()
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+    th = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    [t.start() for t in th]
+    [t.join(timeout=120) for t in th]
+    assert not any(t.is_alive() for t in th), "a rank blocked after its peer failed"
+    assert errs[0] is not None and "fail" in str(errs[0]), errs
+    if how == "bad_ingest":
+        assert errs[1] is not None
+    for c in ctxs:
+        c.close()
+
+
+def test_two_rank_context_without_comm_counts_no_pieces(monkeypatch):
+    # a context of 2 ranks without a communicator (the caller-driven exchange:
+    # fk_map / fk_map_emit) maps its input for the caller; it must not count pieces of it (its
+    # input holds the other rank's records too)
+    monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
+    monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
+    fasta = fk.synth_fasta(40_000, 100, 1_000_000, seed=0xE9)
+    with fk.KmerCounter(28, 10, 3, 2048, n_ranks=2, rank=0) as kc:
+        kc.ingest(fasta)
+        counts = kc.map()
+        assert kc.stats()["pieces_counted"] == 0
+        assert sum(counts) == kc.stats()["superkmers"]
+
+
+@pytest.mark.parametrize("world,seq", [(1, 0), (3, 0), (4, 1), (2, 1)])
+def test_local_exchange_ingest_file_range(small_pieces, tmp_path, world, seq):
+    # the rank's split comes from the library (fk_ingest_file_range: FASTdoop-style
+    # splits, positioned reads in pinned windows of 1 MB here) -- ranges start inside records and
+    # header lines; the union of the ranks' bins is bit-exact vs the oracle on the whole file
+    if seq == 0:
+        fasta = b"text before the first header\n" + fk.synth_fasta(20_000, 100, 500_000, seed=0xEA + world)
+    else:
+        import bench
+        fasta = bench.long_sequence_fasta(3_000_000, seed=0xEB + world)
+    path = tmp_path / "in.fa"
+    path.write_bytes(fasta)
+    ctxs = [fk.KmerCounter(28, 10, 3, 2048, sequence_type=seq, n_ranks=world, rank=r) for r in range(world)]
+    fk.comm_init_local(ctxs)
+    errs = [None] * world
+
+    def work(r):
+        try:
+            ctxs[r].ingest_file_range(str(path), window_bytes=1 << 20)
+            ctxs[r].finish()
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join(timeout=300) for t in th]
+    assert errs == [None] * world, errs
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 2048, sequence_type=seq))
