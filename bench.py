@@ -58,16 +58,27 @@ XGMI_LINK_PEAK = 153e9  # per link, both directions (7 links per GPU; prompt / M
 # workload -> (k, m, B, read_len, genome, sequence_type, default FASTA bytes per GPU, description)
 WORKLOADS = {
     "c2": (28, 10, 2048, 100, 100_000_000, 0, 1_000_000_000,
-           "BASELINE configs[1]: k=28 m=10 x=3 B=2048, 1 GB synthetic 100 bp reads per GPU"),
+           "BASELINE configs[1]: k=28 m=10 x=3 B=2048, {gb} synthetic 100 bp reads per GPU"),
     "c3": (28, 10, 8192, 100, 3_000_000_000, 0, 6_250_000_000,
-           "BASELINE configs[2]: k=28 m=10 x=3 B=8192, 6.25 GB synthetic 100 bp reads per GPU "
-           "(3 Gbp virtual genome; 8 GPUs = the 50 GB job)"),
+           "BASELINE configs[2]: k=28 m=10 x=3 B=8192, {gb} synthetic 100 bp reads per GPU "
+           "(3 Gbp virtual genome; 8 GPUs x 6.25 GB = the 50 GB job)"),
     "c4": (55, 12, 8192, 150, 3_000_000_000, 0, 6_250_000_000,
-           "BASELINE configs[3]: k=55 m=12 x=3 B=8192, 6.25 GB synthetic 150 bp reads per GPU"),
+           "BASELINE configs[3]: k=55 m=12 x=3 B=8192, {gb} synthetic 150 bp reads per GPU "
+           "(3 Gbp virtual genome; 8 GPUs x 6.25 GB = the 50 GB job)"),
     "c5": (28, 10, 2048, 0, 0, 1, 1_000_000_000,
-           "BASELINE configs[4] shape: sequenceType=1, one synthetic long record (60-col lines, "
+           "BASELINE configs[4] shape: sequenceType=1, one synthetic long record of {gb} per GPU (60-col lines, "
            "100 x 10 kbp N runs, 5% soft-masked)"),
 }
+
+
+def workload_label(wl: str, fasta_bytes: int) -> str:
+    """config.workload: the workload's description with the FASTA bytes per GPU actually run (a run
+    below the configuration's per-GPU load says so)."""
+    desc, default = WORKLOADS[wl][7], WORKLOADS[wl][6]
+    label = desc.format(gb=f"{fasta_bytes / 1e9:.3g} GB")
+    if fasta_bytes < 0.99 * default:
+        label += f" -- REDUCED: the configuration's per-GPU load is {default / 1e9:.3g} GB"
+    return label
 
 
 def cpu_baseline(sample_bytes: int, k: int, m: int, B: int, read_len: int, genome: int) -> dict:
@@ -331,7 +342,7 @@ def main() -> None:
             "timed_region": "FASTA in pinned host memory -> H2D (segments on a copy stream, the fused map on every "
                             "landed tile; N > 1: every landed piece exchanged over RCCL while the next is copied) -> "
                             "count -> counts resident on the device (write=0)",
-            "config": {"workload": desc, "k": k, "m": m, "x": 3, "B": B, "useHT": int(args.use_ht),
+            "config": {"workload": workload_label(wl, r0.fasta_bytes), "k": k, "m": m, "x": 3, "B": B, "useHT": int(args.use_ht),
                        "sequenceType": seq_type, "fasta_bytes_per_gpu": r0.fasta_bytes, "bases_per_gpu": r0.bases,
                        "parallelism": par},
             "stages_ms": {"h2d": hs["ms_h2d"], "map_overlapped_with_h2d": hs["ms_signature"],

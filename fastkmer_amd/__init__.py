@@ -128,6 +128,7 @@ def lib():
         "fk_map_bin_kmers": (ctypes.c_int, [P, P]),
         "fk_lpt_owners": (ctypes.c_int, [P, I32, I32, P]),
         "fk_set_bin_owners": (ctypes.c_int, [P, P, P]),
+        "fk_bin_owners": (ctypes.c_int, [P, P]),
         "fk_signature_slots": (U64, [P]),
         "fk_signature_counts": (ctypes.c_int, [P, P, U64]),
         "fk_write_bin_signatures": (ctypes.c_int, [P, P, U64, ctypes.c_char_p]),
@@ -136,6 +137,9 @@ def lib():
         "fk_comm_init": (ctypes.c_int, [P, P]),
         "fk_comm_init_local": (ctypes.c_int, [P, I32]),
         "fk_comm_transport": (ctypes.c_char_p, [P]),
+        "fk_comm_allreduce_u64": (ctypes.c_int, [P, P, SZ]),
+        "fk_balance_bins": (ctypes.c_int, [P, ctypes.c_char_p, SZ]),
+        "fk_balance_bins_file": (ctypes.c_int, [P, ctypes.c_char_p, I32, I32, ctypes.c_double]),
         "fk_exchange_plan": (ctypes.c_int, [I32, I32, P, P, U64, P, P, P, P, P]),
         "fk_debug_wave_count": (ctypes.c_int, [I32, I32, I32, ctypes.c_uint32, ctypes.c_uint32, I32, P,
                                                ctypes.c_uint32, P, P, P]),
@@ -314,6 +318,25 @@ class KmerCounter:
         _check(lib().fk_ingest_file_range(self._h, os.fsencode(path), self.n_ranks if world is None else world,
                                           self.rank if rank is None else rank, window_bytes))
 
+    def balance_bins(self, sample: bytes) -> np.ndarray:
+        """Size-aware placement (useCustomPartitioner) for the library's exchange, collective: the
+        ranks' samples mapped, their per-bin k-mers summed, LPT owners installed; returns them."""
+        _check(lib().fk_balance_bins(self._h, sample, len(sample)))
+        return self.bin_owners()
+
+    def balance_bins_file(self, path: str, fraction: float = 0.01, world: int | None = None,
+                          rank: int | None = None) -> np.ndarray:
+        """balance_bins from `fraction` of this rank's split of the file (the reference samples 1 %)."""
+        _check(lib().fk_balance_bins_file(self._h, os.fsencode(path), self.n_ranks if world is None else world,
+                                          self.rank if rank is None else rank, fraction))
+        return self.bin_owners()
+
+    def comm_allreduce(self, v) -> np.ndarray:
+        """Collective: v summed over the job's ranks."""
+        a = np.ascontiguousarray(v, dtype=np.uint64).copy()
+        _check(lib().fk_comm_allreduce_u64(self._h, a.ctypes.data, a.size))
+        return a
+
     def ingest_device(self, ptr: int, n: int) -> None:
         _check(lib().fk_ingest_device(self._h, ctypes.c_void_p(ptr), n, 1))
 
@@ -337,6 +360,12 @@ class KmerCounter:
         """After map(): k-mers per bin (all b bins) of this rank's records."""
         out = np.zeros(self.num_bins, dtype=np.uint64)
         _check(lib().fk_map_bin_kmers(self._h, out.ctypes.data))
+        return out
+
+    def bin_owners(self) -> np.ndarray:
+        """The placement: owner rank of every bin."""
+        out = np.zeros(self.num_bins, dtype=np.int32)
+        _check(lib().fk_bin_owners(self._h, out.ctypes.data))
         return out
 
     def set_bin_owners(self, owner) -> list[int]:

@@ -1388,7 +1388,7 @@ FK_EXPORT int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks
 FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_counts) {
     if (!c || !owner) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
-    if (c->grouped) return set_err(FK_E_STATE, "size-aware placement with grouped emit enabled (disable it first)");
+    if (c->comm && c->xch.open) return set_err(FK_E_STATE, "fk_set_bin_owners inside a job's exchange");
     for (int32_t b = 0; b < c->Bc; ++b)
         if (owner[b] < 0 || (uint32_t)owner[b] >= c->G)
             return set_err(FK_E_INVALID, "owner[%d] = %d is not a rank of %u", b, owner[b], c->G);
@@ -1412,7 +1412,9 @@ FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_
     HIP_TRY(hipMemcpyAsync(c->d_local.p, c->h_bin_lbin.data(), (uint64_t)c->Bc * 4, hipMemcpyHostToDevice, s));
     c->custom_owners = true;
     c->have_result = false;
-    if (c->mapped) {  // the destinations of the mapped records changed
+    if (c->grouped) {  // the (owner, local bin) parts of the grouped emit follow the new owners
+        FK_TRY(fk_set_grouped_emit(c, 1));
+    } else if (c->mapped) {  // the destinations of the mapped records changed
         c->send_counts.assign(c->G, 0);
         if (c->G == 1) {
             c->send_counts[0] = c->nrec;
@@ -1424,6 +1426,12 @@ FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_
     HIP_TRY(hipStreamSynchronize(s));
     if (send_counts)
         for (uint32_t r = 0; r < c->G; ++r) send_counts[r] = c->mapped ? c->send_counts[r] : 0;
+    return FK_OK;
+}
+
+FK_EXPORT int fk_bin_owners(const fk_ctx *c, int32_t *owner) {
+    if (!c || !owner) return set_err(FK_E_INVALID, "null argument");
+    for (int32_t b = 0; b < c->Bc; ++b) owner[b] = c->custom_owners ? c->h_owner[b] : (int32_t)((uint32_t)b % c->G);
     return FK_OK;
 }
 
@@ -2069,14 +2077,21 @@ FK_EXPORT int fk_reduce(fk_ctx *c, const void *d_recv, uint64_t nrecv) {
 FK_EXPORT int fk_set_grouped_emit(fk_ctx *c, int32_t enable) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     DeviceGuard dg_(c->device);
-    if (enable && c->custom_owners)
-        return set_err(FK_E_STATE, "grouped emit needs the default placement (bin %% n_ranks)");
     c->grouped = enable != 0;
     c->mapped = false;
     if (!c->grouped) return FK_OK;
-    c->grp_nlb = (uint32_t)((c->Bc + (int)c->G - 1) / (int)c->G);
     std::vector<uint32_t> table((size_t)c->Bc);
-    for (int32_t b = 0; b < c->Bc; ++b) table[b] = ((uint32_t)b % c->G) * c->grp_nlb + (uint32_t)b / c->G;
+    if (c->custom_owners) {
+        // size-aware placement (fk_set_bin_owners, the same table on every rank): part = owner *
+        // L + the bin's index among its owner's bins in ascending order (the receiver's local bin)
+        std::vector<uint32_t> cnt(c->G, 0);
+        for (int32_t b = 0; b < c->Bc; ++b) table[b] = cnt[c->h_owner[b]]++;
+        c->grp_nlb = std::max(1u, *std::max_element(cnt.begin(), cnt.end()));
+        for (int32_t b = 0; b < c->Bc; ++b) table[b] += (uint32_t)c->h_owner[b] * c->grp_nlb;
+    } else {
+        c->grp_nlb = (uint32_t)((c->Bc + (int)c->G - 1) / (int)c->G);
+        for (int32_t b = 0; b < c->Bc; ++b) table[b] = ((uint32_t)b % c->G) * c->grp_nlb + (uint32_t)b / c->G;
+    }
     FK_TRY(ensure(c->grp_table, (uint64_t)c->Bc * 4));
     HIP_TRY(hipMemcpy(c->grp_table.p, table.data(), (uint64_t)c->Bc * 4, hipMemcpyHostToDevice));
     return FK_OK;
@@ -2853,7 +2868,6 @@ FK_EXPORT int fk_comm_unique_id(uint8_t *id) {
 FK_EXPORT int fk_comm_init(fk_ctx *c, const uint8_t *id) {
     if (!c || !id) return set_err(FK_E_INVALID, "null argument");
     if (c->comm) return set_err(FK_E_STATE, "the context already has a communicator");
-    if (c->custom_owners) return set_err(FK_E_STATE, "the exchange uses the default placement (bin %% n_ranks)");
     DeviceGuard dg_(c->device);
     std::string err;
     fk::Comm *comm = fk::comm_create_rccl(id, (int)c->G, c->cfg.rank, c->device, err);
@@ -2876,7 +2890,6 @@ FK_EXPORT int fk_comm_init_local(fk_ctx **ctxs, int32_t n) {
             return set_err(FK_E_INVALID, "context %d has rank %d of %u; expected rank %d of %d", r, c->cfg.rank, c->G,
                            r, n);
         if (c->comm) return set_err(FK_E_STATE, "context %d already has a communicator", r);
-        if (c->custom_owners) return set_err(FK_E_STATE, "the exchange uses the default placement (bin %% n_ranks)");
         devs[r] = c->device;
     }
     std::vector<fk::Comm *> comms(n, nullptr);
@@ -2896,6 +2909,117 @@ FK_EXPORT int fk_comm_init_local(fk_ctx **ctxs, int32_t n) {
 }
 
 FK_EXPORT const char *fk_comm_transport(const fk_ctx *c) { return c && c->comm ? c->comm->kind() : ""; }
+
+FK_EXPORT int fk_comm_allreduce_u64(fk_ctx *c, uint64_t *v, size_t n) {
+    if (!c || (!v && n)) return set_err(FK_E_INVALID, "null argument");
+    if (!c->comm) return set_err(FK_E_STATE, "fk_comm_allreduce_u64 needs a communicator (fk_comm_init*)");
+    DeviceGuard dg_(c->device);
+    std::string err;
+    if (c->comm->allreduce_sum_u64(v, n, c->comm_stream, err)) return comm_fail(c, set_err(FK_E_DEVICE, "%s", err.c_str()));
+    return FK_OK;
+}
+
+// ---- size-aware placement on the library's exchange (useCustomPartitioner, SBKC:1023-1026 and
+// MultiprocessorSchedulingPartitioner.scala:35-69): every rank maps a sample of its input (no
+// exchange), the per-bin k-mer totals are summed over the ranks (the reduceByKey of :1024), the
+// LPT placement is computed identically on every rank and installed for the job's exchange.
+static int sample_bin_kmers(fk_ctx *c, const uint8_t *sample, size_t n, std::vector<uint64_t> &sizes) {
+    if (c->comm && c->xch.open) return set_err(FK_E_STATE, "bin placement inside a job's exchange");
+    sizes.assign((size_t)c->Bc, 0);
+    fk::Comm *comm = c->comm;
+    c->comm = nullptr;  // the sample is mapped here, never exchanged
+    int rc = n ? ingest_impl(c, sample, n, 1) : FK_OK;
+    if (!rc && n) rc = map_records(c);
+    if (!rc && n && c->nrec) {
+        rc = part_count(c->binhist, map_src(c), 1, 1, nullptr, (uint32_t)c->Bc, c->ws, c->stream);
+        if (!rc) {
+            hipError_t e = hipMemcpyAsync(sizes.data(), c->binhist.kmer.p, (uint64_t)c->Bc * 8, hipMemcpyDeviceToHost,
+                                          c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) rc = set_err(FK_E_DEVICE, "sample histogram: %s", hipGetErrorString(e));
+        }
+    }
+    c->comm = comm;
+    c->ingest_fresh = true;
+    c->mapped = false;
+    c->have_result = false;
+    return rc;
+}
+
+static int balance_from_sample(fk_ctx *c, const uint8_t *sample, size_t n) {
+    DeviceGuard dg_(c->device);
+    std::vector<uint64_t> sizes;
+    FK_TRY(sample_bin_kmers(c, sample, n, sizes));
+    if (c->comm) {
+        std::string err;
+        if (c->comm->allreduce_sum_u64(sizes.data(), sizes.size(), c->comm_stream, err))
+            return set_err(FK_E_DEVICE, "bin size all-reduce: %s", err.c_str());
+    }
+    std::vector<int32_t> owner((size_t)c->Bc);
+    FK_TRY(fk_lpt_owners(sizes.data(), c->Bc, (int32_t)c->G, owner.data()));
+    return fk_set_bin_owners(c, owner.data(), nullptr);
+}
+
+FK_EXPORT int fk_balance_bins(fk_ctx *c, const uint8_t *sample, size_t n) {
+    if (!c || (!sample && n)) return set_err(FK_E_INVALID, "null argument");
+    const int rc = balance_from_sample(c, sample, n);
+    return rc && c->comm ? comm_fail(c, rc) : rc;
+}
+
+// The sample of a file split: `fraction` of the rank's split as evenly spaced blocks of whole
+// records (sequenceType 0) or of sequence (1, each block one record), the reference's
+// sample(false, 0.01) of SBKC:1024 taken as blocks of the rank's own input.
+static int split_sample(const char *path, int32_t world, int32_t rank, int32_t k, int32_t seq, double fraction,
+                        std::vector<uint8_t> &out) {
+    out.clear();
+    Fd f;
+    uint64_t size = 0;
+    SplitPlan plan;
+    FK_TRY(open_split(path, world, rank, k, seq, f, size, plan));
+    if (plan.total == 0 || fraction <= 0.0) return FK_OK;
+    std::vector<uint8_t> piece;
+    std::string err;
+    if (fraction >= 1.0) {
+        out.resize(plan.total);
+        if (read_split(f.fd, size, plan, 0, plan.total, out.data(), err)) return set_err(FK_E_IO, "%s", err.c_str());
+        return FK_OK;
+    }
+    constexpr uint64_t BLOCK = 1ull << 20;
+    const uint64_t want = std::max<uint64_t>((uint64_t)((double)plan.total * fraction), 1);
+    const uint64_t nblk = std::max<uint64_t>(1, (want + BLOCK - 1) / BLOCK);
+    const uint64_t blk = std::min<uint64_t>(plan.total, std::max<uint64_t>(4096, want / nblk));
+    std::vector<uint8_t> buf;
+    for (uint64_t i = 0; i < nblk; ++i) {
+        const uint64_t at = plan.total * i / nblk, len = std::min(blk, plan.total - at);
+        buf.resize(len);
+        if (read_split(f.fd, size, plan, at, len, buf.data(), err)) return set_err(FK_E_IO, "%s", err.c_str());
+        if (seq == 0) {  // whole records: from the first '>' opening a line to the last record start
+            size_t a = 0;
+            while (a < buf.size() && !(buf[a] == '>' && (a == 0 ? at == 0 : buf[a - 1] == '\n'))) ++a;
+            size_t e = buf.size();
+            if (at + len < plan.total) {
+                while (e > a + 1 && !(buf[e - 1] == '>' && buf[e - 2] == '\n')) --e;
+                e = e > a + 1 ? e - 1 : a;
+            }
+            out.insert(out.end(), buf.begin() + a, buf.begin() + e);
+        } else {  // a block of the sequence as one record
+            const uint8_t h[3] = {'\n', '>', '\n'};
+            out.insert(out.end(), h, h + 3);
+            out.insert(out.end(), buf.begin(), buf.end());
+        }
+    }
+    if (seq == 1) out.push_back('\n');
+    if (seq == 1 && !out.empty()) out.erase(out.begin());  // the first block's header starts the input
+    return FK_OK;
+}
+
+FK_EXPORT int fk_balance_bins_file(fk_ctx *c, const char *path, int32_t world, int32_t rank, double fraction) {
+    if (!c || !path) return set_err(FK_E_INVALID, "null argument");
+    std::vector<uint8_t> sample;
+    int rc = split_sample(path, world, rank, c->cfg.k, c->cfg.sequence_type, fraction, sample);
+    if (!rc) rc = balance_from_sample(c, sample.data(), sample.size());
+    return rc && c->comm ? comm_fail(c, rc) : rc;
+}
 
 // ---------------------------------------------------------------------------
 // results

@@ -193,10 +193,14 @@ int fk_finish(fk_ctx *ctx);
  *   fk_lpt_owners: largest bin first onto the least loaded rank (host only;
  *     bins of size 0 keep bin % n_ranks),
  *   fk_set_bin_owners: install owner[b] (the same table on every rank) before
- *     fk_map_emit / fk_reduce; recomputes send_counts when already mapped. */
+ *     fk_map_emit / fk_reduce, or before a job's first fk_ingest with a
+ *     communicator (the exchange then groups records by (owner, the bin's index
+ *     among its owner's bins)); recomputes send_counts when already mapped. */
 int fk_map_bin_kmers(fk_ctx *ctx, uint64_t *kmers_per_bin);
 int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks, int32_t *owner);
 int fk_set_bin_owners(fk_ctx *ctx, const int32_t *owner, uint64_t *send_counts);
+/* The context's placement: owner[b] for all b bins (bin % n_ranks unless set). */
+int fk_bin_owners(const fk_ctx *ctx, int32_t *owner);
 
 /* ---- multi-GPU inside the context (one context per GPU) --------
  * The job's contexts (fk_config.n_ranks = n, rank = 0..n-1) join one
@@ -220,6 +224,20 @@ int fk_comm_init(fk_ctx *ctx, const uint8_t id[FK_COMM_ID_BYTES]);
 int fk_comm_init_local(fk_ctx **ctxs, int32_t n);
 /* "rccl", "local" or "" (no communicator). */
 const char *fk_comm_transport(const fk_ctx *ctx);
+/* Collective: v[0..n) summed over the job's ranks (in place). */
+int fk_comm_allreduce_u64(fk_ctx *ctx, uint64_t *v, size_t n);
+/* Size-aware placement for the library's exchange (useCustomPartitioner:
+ * SBKC:1023-1026, MultiprocessorSchedulingPartitioner.scala:35-69), collective,
+ * before a job's first fk_ingest: every rank maps a sample of its input (never
+ * exchanged), the per-bin k-mer totals are summed over the ranks, and the LPT
+ * placement (fk_lpt_owners) is installed on every rank (fk_set_bin_owners);
+ * the job's records then go to their bin's owner.  Without a communicator the
+ * rank's own sample decides.
+ *   fk_balance_bins: the caller's sample bytes (FASTA text);
+ *   fk_balance_bins_file: `fraction` of the rank's split of the file (evenly
+ *     spaced blocks; the reference samples 1 %). */
+int fk_balance_bins(fk_ctx *ctx, const uint8_t *sample, size_t n);
+int fk_balance_bins_file(fk_ctx *ctx, const char *path, int32_t world, int32_t rank, double fraction);
 /* Host-only arithmetic of one exchange step.  sent[d * (2 * parts + 1) + i] is this
  * rank's message to rank d: records of local bin i (i < parts), k-mers of local bin
  * i - parts, then a flag word (bit 0: the sender's last piece, bit 1: the sender

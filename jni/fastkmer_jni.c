@@ -70,6 +70,20 @@ JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_ingest(JNIEnv *env, 
     if (rc != FK_OK) throw_fk(env, rc);
 }
 
+/* def ingestFileRange(h, path, world, rank, window): Unit -- the job's whole input: this rank's
+ * split of the file (FASTdoop-style: whole records for sequenceType 0, the k - 1 overlap and a
+ * header prefix for sequenceType 1; SBKC:993, 1009-1012), read by the library in pinned windows */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_ingestFileRange(JNIEnv *env, jobject self, jlong h,
+                                                                           jstring path, jint world, jint rank,
+                                                                           jlong window) {
+    (void)self;
+    const char *p = (*env)->GetStringUTFChars(env, path, NULL);
+    if (!p) return;
+    const int rc = fk_ingest_file_range(ctx_of(h), p, world, rank, window < 0 ? 0 : (uint64_t)window);
+    (*env)->ReleaseStringUTFChars(env, path, p);
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
 /* def finish(h): Unit -- map and count (one rank); with a communicator the last piece, the
  * exchange with the other ranks and the count of this rank's bins (collective) */
 JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_finish(JNIEnv *env, jobject self, jlong h) {

@@ -11,9 +11,6 @@
  */
 package skc.gpu
 
-import java.nio.channels.FileChannel
-import java.nio.file.{Paths, StandardOpenOption}
-
 import skc.test.testutil.TestConfiguration
 
 object NativeKmerCounter {
@@ -22,6 +19,7 @@ object NativeKmerCounter {
   @native def create(k: Int, m: Int, x: Int, b: Int, useHT: Boolean, sequenceType: Int,
                      nRanks: Int, rank: Int, device: Int): Long
   @native def ingest(h: Long, fasta: java.nio.ByteBuffer, n: Long, last: Boolean): Unit
+  @native def ingestFileRange(h: Long, path: String, world: Int, rank: Int, window: Long): Unit
   @native def finish(h: Long): Unit
   @native def commUniqueId(): Array[Byte]
   @native def commInit(h: Long, id: Array[Byte]): Unit
@@ -30,22 +28,12 @@ object NativeKmerCounter {
   @native def findBinSignatures(h: Long, outDir: String): Unit
   @native def destroy(h: Long): Unit
 
-  /** The file is streamed in mapped windows of `window` bytes (fk_ingest appends them). */
-  private def ingestFile(h: Long, dataset: String, window: Long): Unit = {
-    val ch = FileChannel.open(Paths.get(dataset), StandardOpenOption.READ)
-    try {
-      val size = ch.size()
-      if (size == 0L) ingest(h, java.nio.ByteBuffer.allocateDirect(0), 0L, true)
-      var off = 0L
-      while (off < size) {
-        val len = math.min(window, size - off)
-        ingest(h, ch.map(FileChannel.MapMode.READ_ONLY, off, len), len, off + len >= size)
-        off += len
-      }
-    } finally ch.close()
-  }
+  /** The whole file as the job's input, read by the library (fk_ingest_file_range: positioned
+    * reads into pinned windows, each copied and mapped while the next is read). */
+  private def ingestFile(h: Long, dataset: String, window: Long): Unit =
+    ingestFileRange(h, dataset, 1, 0, window)
 
-  def executeJob(configuration: TestConfiguration, device: Int = -1, window: Long = 1L << 30): Unit = {
+  def executeJob(configuration: TestConfiguration, device: Int = -1, window: Long = 1L << 28): Unit = {
     val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
       configuration.useHT, configuration.sequenceType, 1, 0, device)
     try {
@@ -56,21 +44,20 @@ object NativeKmerCounter {
   }
 
   /** One rank of an nRanks-GPU job (one executor per GPU): `commId` comes from commUniqueId()
-    * on one node and reaches every rank with the task (a broadcast variable); `split` is this
-    * rank's input -- (path, offset, length) of its byte range plus the k - 1 overlap, as the
-    * FASTdoop input splits of SBKC:1009-1012 cut it.  The records move between the GPUs inside
-    * finish (RCCL all-to-all over xGMI, the reduceByKey of :1034-1042); each rank writes the
-    * bin files of the bins it owns (bin % nRanks == rank) into the shared output directory. */
+    * on one node and reaches every rank with the task (a broadcast variable).  The rank reads its
+    * own split of `configuration.dataset` -- the library cuts it as FASTdoop's input formats do
+    * (SBKC:993, 1009-1012): whole records for sequenceType 0; for sequenceType 1 the rank's byte
+    * range with a header prefix and the k - 1 overlap -- and streams it in windows of `window`
+    * bytes (any split size: no 2 GiB mapping limit).  The records move between the GPUs inside
+    * ingest / finish (RCCL all-to-all over xGMI, the reduceByKey of :1034-1042); each rank writes
+    * the bin files of the bins it owns (bin % nRanks == rank) into the shared output directory. */
   def executeJobRank(configuration: TestConfiguration, rank: Int, nRanks: Int, commId: Array[Byte],
-                     split: (String, Long, Long), device: Int = -1): Array[Long] = {
+                     device: Int = -1, window: Long = 1L << 28): Array[Long] = {
     val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
       configuration.useHT, configuration.sequenceType, nRanks, rank, device)
     try {
       commInit(h, commId)
-      val (path, off, len) = split
-      val ch = FileChannel.open(Paths.get(path), StandardOpenOption.READ)
-      try ingest(h, ch.map(FileChannel.MapMode.READ_ONLY, off, len), len, true)
-      finally ch.close()
+      ingestFileRange(h, configuration.dataset, nRanks, rank, window)
       finish(h)
       if (configuration.write) writeBins(h, configuration.outputDir)
       binSizes(h)
@@ -79,7 +66,7 @@ object NativeKmerCounter {
 
   /** SparkBinKmerCounter.executeFindBinSignaturesJob (:956-986): bin_signatures<b>.txt. */
   def executeFindBinSignaturesJob(configuration: TestConfiguration, device: Int = -1,
-                                  window: Long = 1L << 30): Unit = {
+                                  window: Long = 1L << 28): Unit = {
     val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
       configuration.useHT, configuration.sequenceType, 1, 0, device)
     try {

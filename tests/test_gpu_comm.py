@@ -77,19 +77,21 @@ def run_local_job(shards, k, m, x=3, B=2048, use_ht=False, seq=0, feed="bytes", 
     return ctxs
 
 
-def assert_union_matches_oracle(ctxs, ref, ordered=True):
+def assert_union_matches_oracle(ctxs, ref, ordered=True, owner=None):
+    """owner: the bin -> rank placement (default bin % G)"""
     G = len(ctxs)
     ref_sizes = ref.bin_sizes()
     total = np.zeros(ref.nbins, dtype=np.int64)
+    owner = np.arange(ref.nbins) % G if owner is None else np.asarray(owner)
     for r, kc in enumerate(ctxs):
         sizes = kc.bin_sizes().astype(np.int64)
-        own = np.arange(ref.nbins) % G == r
+        own = owner == r
         assert np.all(sizes[~own] == 0), f"rank {r} holds bins it does not own"
         total += sizes
     bad = np.nonzero(total != ref_sizes)[0]
     assert len(bad) == 0, f"bin sizes differ in {len(bad)} bins, e.g. {bad[:5]}"
     for b in np.nonzero(ref_sizes)[0].tolist():
-        hi, lo, cnt = counter_arrays(ctxs[b % G], b)
+        hi, lo, cnt = counter_arrays(ctxs[int(owner[b])], b)
         rhi, rlo, rcnt = ref.bin_arrays(b)
         if not ordered:
             order = np.lexsort((lo, hi))
@@ -354,3 +356,43 @@ def test_local_exchange_ingest_file_range(small_pieces, tmp_path, world, seq):
     [t.join(timeout=300) for t in th]
     assert errs == [None] * world, errs
     assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 2048, sequence_type=seq))
+
+
+@pytest.mark.parametrize("use_ht,k,m", [(False, 28, 10), (True, 28, 10), (False, 55, 12)])
+def test_local_exchange_size_aware_placement(small_pieces, tmp_path, use_ht, k, m):
+    # useCustomPartitioner (SBKC:1023-1026, MultiprocessorSchedulingPartitioner
+    # .scala:35-69) on the library's exchange: 4 ranks sample their splits (fk_balance_bins_file),
+    # the per-bin k-mer totals are all-reduced and LPT owners installed on every rank, then the job
+    # runs through the native exchange.  Skewed input: a third of the reads come from a 30 kbp
+    # region (its bins hold far more k-mers).  Bit-exact vs the oracle under the LPT owners.
+    G = 4
+    rl = 100 if k == 28 else 150
+    fasta = fk.synth_fasta(16_000, rl, 2_000_000, seed=0xF2) + \
+        fk.synth_fasta(8_000, rl, 30_000, seed=0xF3, first_read=16_000)
+    path = tmp_path / "skewed.fa"
+    path.write_bytes(fasta)
+    ctxs = [fk.KmerCounter(k, m, 3, 2048, use_ht, n_ranks=G, rank=r) for r in range(G)]
+    fk.comm_init_local(ctxs)
+    owners, errs = [None] * G, [None] * G
+
+    def work(r):
+        try:
+            owners[r] = ctxs[r].balance_bins_file(str(path), fraction=0.25)
+            ctxs[r].ingest_file_range(str(path))
+            ctxs[r].finish()
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+    th = [threading.Thread(target=work, args=(r,)) for r in range(G)]
+    [t.start() for t in th]
+    [t.join(timeout=300) for t in th]
+    assert errs == [None] * G, errs
+    assert all(np.array_equal(o, owners[0]) for o in owners), "ranks disagree on the placement"
+    owner = owners[0]
+    assert not np.array_equal(owner, np.arange(2048) % G), "LPT placement equals the default"
+    ref = oracle.OracleResult(fasta, k, m, 2048)
+    assert_union_matches_oracle(ctxs, ref, ordered=not use_ht, owner=owner)
+    # the placement balances the ranks' k-mers better than bin % G on this input
+    km = np.array([int(ref.bin_arrays(b)[2].sum(dtype=np.uint64)) for b in range(2048)], dtype=np.int64)
+    lpt = max(km[owner == r].sum() for r in range(G))
+    default = max(km[np.arange(2048) % G == r].sum() for r in range(G))
+    assert lpt <= default * 1.02, (lpt, default)
