@@ -341,6 +341,15 @@ struct fk_ctx {
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
     bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
+    // The sorted count's result is bucket-major ("gapped"): bucket q's distinct keys ascending at its
+    // first slot buckets[q].begin of res_keys / out_counts, dense_off[q] = their exclusive offset in the
+    // bin-ordered result, bin_off / h_bin_off per bin.  Readers gather a bin's buckets (fk_get_bin) or
+    // the whole result (fk_write_bins); the pieces merged by count_piece need dense arrays (want_dense).
+    bool gapped = false, dense_ready = false, want_dense = false;
+    const uint64_t *res_keys = nullptr;   // okb of the last sorted count (out_keys, or mid)
+    uint64_t res_nbuckets = 0;
+    int res_F = 0;
+    DevBuf gather_keys, gather_counts;    // fk_get_bin's gather of one bin
 
     // multi-rank exchange inside the context (fk_comm_init / fk_comm_init_local): the input
     // is emitted in pieces grouped by (destination, local bin) and each piece is exchanged
@@ -651,7 +660,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
-                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_total};
+                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -719,6 +728,7 @@ FK_EXPORT int32_t fk_num_bins(const fk_ctx *c) { return c ? c->Bc : 0; }
 static void reset_results(fk_ctx *c) {
     c->mapped = false;
     c->have_result = false;
+    c->gapped = c->dense_ready = false;
     c->distinct = 0;
     c->h_bin_off.clear();
 }
@@ -1569,6 +1579,10 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     const bool tiered = pl.tiered;
     const uint32_t cap = pl.cap, wave_cap = pl.wave_cap;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
+    // the one-array count writes its buckets' results over the first expansion level (`mid` is dead
+    // once level 2 has run, stream order): one k-mer array less on the device (57 GB at configs[3]'s
+    // per-GPU load, 128-bit keys)
+    DevBuf &okb = (src_in.np == 0 && pl.two_level && c->mid.bytes >= total_kmers * 8 * c->KW) ? c->mid : c->out_keys;
     FK_TRY(ensure(c->flags, ncell_all * 4));
     FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
@@ -1589,7 +1603,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     HIP_TRY(hipStreamSynchronize(s));
     htrace("sorted: nbuckets read");
     FK_TRY(ensure(c->buckets, nbuckets * sizeof(Bucket)));
-    FK_TRY(ensure(c->out_keys, total_kmers * 8 * c->KW));
+    FK_TRY(ensure(okb, total_kmers * 8 * c->KW));
     FK_TRY(ensure(c->out_counts, total_kmers * 4));
     FK_TRY(ensure(c->bucket_unique, (nbuckets + 1) * 8));
     FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
@@ -1619,12 +1633,12 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
-                                               c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                               okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                                c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
                                                nullptr, s));
         else
             HIP_TRY(launch_bucket_count128_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
-                                                c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                                okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                                 c->bucket_unique.as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
                                                 s));
         HIP_TRY(hipEventSynchronize(c->tier_ev));
@@ -1632,19 +1646,19 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         htrace("sorted: tiers read");
         if (ntier[0] && c->KW == 1)
             HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), ntier[0], k,
-                                          c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                          okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
                                           cap, 99, lists, s));
         else if (ntier[0])
             HIP_TRY(launch_bucket_sort(2, src, c->buckets.as<Bucket>(), ntier[0], k,
-                                       c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                       okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, s));
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
             // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
             HIP_TRY(launch_bucket_count64_big(src, c->buckets.as<Bucket>(), ntier[1], k,
-                                              c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                              okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                               c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
                                               lists + nbuckets, s));
             HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
@@ -1653,7 +1667,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         if (nlarge) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
             HIP_TRY(launch_bucket_sort_large(c->KW, src, c->buckets.as<Bucket>(), ntier[1], k,
-                                             c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
+                                             c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              lists + nbuckets, s));
         }
@@ -1662,12 +1676,12 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         if (src.np > 0) return set_err(FK_E_INVALID, "staged pieces need the tiered count");
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), nbuckets, k,
-                                          c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                          okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                           c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
                                           small_limit, c->dbg_phase, nullptr, s));
         else
             HIP_TRY(launch_bucket_sort(c->KW, src, c->buckets.as<Bucket>(), nbuckets, k,
-                                       c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+                                       okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                        c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
                                        small_limit, nullptr, s));
         uint64_t oversize = 0;
@@ -1677,13 +1691,27 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         if (oversize) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
             HIP_TRY(launch_bucket_sort_large(c->KW, src, c->buckets.as<Bucket>(), nbuckets, k,
-                                             c->scratch.as<uint64_t>(), c->out_keys.as<uint64_t>(),
+                                             c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                              c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
                                              nullptr, s));
         }
     }
     HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
+    FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
+    c->distinct_pending = true;
+    if (!c->want_dense) {
+        // the result stays bucket-major (no compaction pass): the buckets' outputs are the result
+        HIP_TRY(launch_bin_offsets(c->flag_scan.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
+                                   c->bin_off.as<uint64_t>(), s));
+        c->gapped = true;
+        c->dense_ready = false;
+        c->res_keys = okb.as<uint64_t>();
+        c->res_nbuckets = nbuckets;
+        c->res_F = F;
+        return FK_OK;
+    }
+    c->gapped = false;
     // the dense result sized for every key (a bound on the distinct keys) when that is at most a
     // tenth of the device and fits twice over in its free memory: the compaction is then queued without waiting for the distinct total,
     // which arrives with the bin offsets (resolve_distinct); else the total is read first
@@ -1709,13 +1737,11 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
         FK_TRY(ensure(c->dense_counts, distinct * 4));
     }
-    FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
-    HIP_TRY(launch_bucket_compact(c->KW, c->out_keys.as<uint64_t>(), c->out_counts.as<uint32_t>(),
+    HIP_TRY(launch_bucket_compact(c->KW, okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
                                   c->buckets.as<Bucket>(), nbuckets, c->dense_off.as<uint64_t>(),
                                   c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(), s));
     HIP_TRY(launch_bin_offsets(c->flag_scan.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
                                c->bin_off.as<uint64_t>(), s));
-    c->distinct_pending = true;
     return FK_OK;
 }
 
@@ -2274,7 +2300,10 @@ template <class F>
 static int count_piece(fk_ctx *c, F count, bool last) {
     htrace("count_piece: enter");
     swap_result(c, c->tmp);
+    c->want_dense = true;  // piece results are merged (fk_merge.inc reads dense arrays)
     const int rc = count();
+    c->want_dense = false;
+    c->gapped = false;
     swap_result(c, c->tmp);
     if (rc) return rc;
     c->acc_ms_part += c->stats.ms_partition;
@@ -3045,6 +3074,36 @@ FK_EXPORT int fk_bin_sizes(fk_ctx *c, uint64_t *out) {
     return FK_OK;
 }
 
+// A bucket-major result made dense (fk_write_bins): the buckets' outputs compacted in bin order.
+static int materialize_dense(fk_ctx *c) {
+    if (!c->gapped || c->dense_ready) return FK_OK;
+    hipStream_t s = c->stream;
+    FK_TRY(ensure(c->dense_keys, c->distinct * 8 * c->KW));
+    FK_TRY(ensure(c->dense_counts, c->distinct * 4));
+    HIP_TRY(launch_bucket_compact(c->KW, c->res_keys, c->out_counts.as<uint32_t>(), c->buckets.as<Bucket>(),
+                                  c->res_nbuckets, c->dense_off.as<uint64_t>(), c->dense_keys.as<uint64_t>(),
+                                  c->dense_counts.as<uint32_t>(), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->dense_ready = true;
+    return FK_OK;
+}
+
+// One local bin of a bucket-major result into dst (device): its buckets [q0, q1) -- the bin's first
+// cell starts a bucket, so q0 = flag_scan[lb << F] -- compacted at dense_off[q] - dense_off[q0].
+static int gather_bin(fk_ctx *c, uint32_t lb, uint64_t *dkeys, uint32_t *dcounts) {
+    hipStream_t s = c->stream;
+    uint64_t q[2] = {0, c->res_nbuckets};
+    const uint64_t *fs = c->flag_scan.as<uint64_t>();
+    HIP_TRY(hipMemcpyAsync(&q[0], fs + ((uint64_t)lb << c->res_F), 8, hipMemcpyDeviceToHost, s));
+    if (lb + 1 < c->nlb) HIP_TRY(hipMemcpyAsync(&q[1], fs + ((uint64_t)(lb + 1) << c->res_F), 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t d0 = c->h_bin_off[lb];
+    if (q[1] > q[0])
+        HIP_TRY(launch_bucket_compact(c->KW, c->res_keys, c->out_counts.as<uint32_t>(), c->buckets.as<Bucket>() + q[0],
+                                      q[1] - q[0], c->dense_off.as<uint64_t>() + q[0], dkeys - d0 * c->KW, dcounts - d0, s));
+    return FK_OK;
+}
+
 FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *counts, size_t cap, size_t *n) {
     if (!c || !n) return set_err(FK_E_INVALID, "null argument");
     DeviceGuard dg_(c->device);
@@ -3059,6 +3118,16 @@ FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *count
     *n = (size_t)cnt;
     if (cnt == 0) return FK_OK;
     if (cap < cnt) return set_err(FK_E_RANGE, "bin %d has %llu k-mers, buffer holds %zu", bin, (unsigned long long)cnt, cap);
+    if (c->gapped && !c->dense_ready) {
+        FK_TRY(ensure(c->gather_keys, cnt * 8 * c->KW));
+        FK_TRY(ensure(c->gather_counts, cnt * 4));
+        FK_TRY(gather_bin(c, lb, c->gather_keys.as<uint64_t>(), c->gather_counts.as<uint32_t>()));
+        if (keys)
+            HIP_TRY(hipMemcpyAsync(keys, c->gather_keys.p, cnt * 8 * c->KW, hipMemcpyDeviceToHost, c->stream));
+        if (counts) HIP_TRY(hipMemcpyAsync(counts, c->gather_counts.p, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return FK_OK;
+    }
     if (keys)
         HIP_TRY(hipMemcpy(keys, c->dense_keys.as<uint64_t>() + b0 * c->KW, cnt * 8 * c->KW, hipMemcpyDeviceToHost));
     if (counts) HIP_TRY(hipMemcpy(counts, c->dense_counts.as<uint32_t>() + b0, cnt * 4, hipMemcpyDeviceToHost));
@@ -3144,6 +3213,7 @@ FK_EXPORT int fk_write_bins(fk_ctx *c, const char *out_dir) {
     const uint32_t nlb = c->nlb;
     const int eof = c->cfg.use_ht == 0;
     if (D == 0) return FK_OK;  // no k-mers: no bin files
+    FK_TRY(materialize_dense(c));
     DevBuf len, off, bbytes, text;
     struct Free {
         DevBuf *b[4];
