@@ -347,6 +347,7 @@ struct fk_ctx {
     // the whole result (fk_write_bins); the pieces merged by count_piece need dense arrays (want_dense).
     bool gapped = false, dense_ready = false, want_dense = false;
     const uint64_t *res_keys = nullptr;   // okb of the last sorted count (out_keys, or mid)
+    const uint64_t *res_fs = nullptr;     // flag_scan of its bucket cut
     uint64_t res_nbuckets = 0;
     int res_F = 0;
     DevBuf gather_keys, gather_counts;    // fk_get_bin's gather of one bin
@@ -387,6 +388,17 @@ struct fk_ctx {
     uint64_t st_kmers = 0;                       // k-mers expanded so far
     DevBuf st_keys[STAGE_MAXP], st_cb[STAGE_MAXP], st_total, piece_starts;
     int st_starts = 1;                           // FASTKMER_STAGED_STARTS=0: the wave tier reads st_cb itself
+    // pre-count (k <= 32, one rank, staged): once pre_at pieces are expanded, their buckets are counted
+    // while the rest lands; the final count merges those results with the later pieces' raw keys
+    // (FASTKMER_PRECOUNT: 1 always, 0 never, -1 (default) when the last job was redundant)
+    int precount = -1;
+    uint32_t pre_at = 2;
+    bool pre_done = false;
+    uint32_t pre_np = 0;
+    uint64_t pre_nb = 0, pre_kmers = 0;
+    DevBuf pre_total, pre_base, pre_flags, pre_flag_scan, pre_buckets, pre_unique, pre_tier_list, pre_piece_starts,
+        pre_keys, pre_counts;
+    hipEvent_t pre_ev[2] = {nullptr, nullptr};
     hipEvent_t st_ev[4 * STAGE_MAXP] = {};       // per piece: partition begin / end, expansion begin / end
 
     fk::Comm *comm = nullptr;
@@ -588,6 +600,9 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *pm = getenv("FASTKMER_PIECE_MODE"); pm && pm[0]) c->piece_mode = atoi(pm);
     if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
     if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
+    if (const char *pc = getenv("FASTKMER_PRECOUNT"); pc && pc[0]) c->precount = atoi(pc);
+    if (const char *pa = getenv("FASTKMER_PRECOUNT_AT"); pa && pa[0])
+        c->pre_at = (uint32_t)std::max(1, std::min(STAGE_MAXP - 1, atoi(pa)));
     if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
         c->ingest_seg = std::max(1ull << 16, strtoull(sg, nullptr, 10));
     const char *cm = getenv("FASTKMER_COUNT_MODE");
@@ -624,6 +639,13 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         return set_err(FK_E_DEVICE, "copy stream / events: %s", hipGetErrorString(e));
     }
     for (auto &ev : c->ev) {
+        e = hipEventCreate(&ev);
+        if (e != hipSuccess) {
+            fk_destroy(c);
+            return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
+        }
+    }
+    for (auto &ev : c->pre_ev) {
         e = hipEventCreate(&ev);
         if (e != hipSuccess) {
             fk_destroy(c);
@@ -702,6 +724,11 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     for (int p = 0; p < STAGE_MAXP; ++p) release(c->st_keys[p]), release(c->st_cb[p]);
     release(c->st_total);
     release(c->piece_starts);
+    for (DevBuf *b : {&c->pre_total, &c->pre_base, &c->pre_flags, &c->pre_flag_scan, &c->pre_buckets, &c->pre_unique,
+                      &c->pre_tier_list, &c->pre_piece_starts, &c->pre_keys, &c->pre_counts})
+        release(*b);
+    for (auto &ev : c->pre_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (c->seg_ev) (void)hipEventDestroy(c->seg_ev);
     for (auto &ev : c->h2d_ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1572,48 +1599,56 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
 
 // 4c + 5: buckets over c->cell_total / c->cell_base (the job's cells), their exact counts from
 // `src` (one key array, or the staged pieces'), the dense result and its bin offsets
-static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in, uint64_t total_kmers) {
+// The buffers of one bucket cut and its counts (the job's, or a staged job's pre-count).
+struct CountBufs {
+    DevBuf *flags, *flag_scan, *buckets, *bucket_unique, *tier_list, *piece_starts, *out_counts;
+};
+static CountBufs main_bufs(fk_ctx *c) {
+    return CountBufs{&c->flags, &c->flag_scan, &c->buckets, &c->bucket_unique, &c->tier_list, &c->piece_starts,
+                     &c->out_counts};
+}
+
+// 4c + 5: buckets over cell_total / cell_base (ncell_all cells), their exact counts from `src` (one
+// key array, or the staged pieces') into okb / B.out_counts at each bucket's first slot, the
+// distinct keys per bucket in B.bucket_unique; *nb_out = buckets
+static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in, uint64_t total_kmers,
+                                const uint64_t *cell_total, const uint64_t *cell_base, CountBufs B, DevBuf &okb,
+                                uint64_t *nb_out) {
     hipStream_t s = c->stream;
     const int k = c->cfg.k;
     const int F = pl.F;
     const bool tiered = pl.tiered;
     const uint32_t cap = pl.cap, wave_cap = pl.wave_cap;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
-    // the one-array count writes its buckets' results over the first expansion level (`mid` is dead
-    // once level 2 has run, stream order): one k-mer array less on the device (57 GB at configs[3]'s
-    // per-GPU load, 128-bit keys)
-    DevBuf &okb = (src_in.np == 0 && pl.two_level && c->mid.bytes >= total_kmers * 8 * c->KW) ? c->mid : c->out_keys;
-    FK_TRY(ensure(c->flags, ncell_all * 4));
-    FK_TRY(ensure(c->flag_scan, (ncell_all + 1) * 8));
+    FK_TRY(ensure(*B.flags, ncell_all * 4));
+    FK_TRY(ensure(*B.flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
     // 4c: buckets.  Tiered (k <= 32): cells packed greedily into buckets of
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(c->cell_total.as<uint64_t>(), c->nlb, F,
+        HIP_TRY(launch_bucket_flags_greedy(cell_total, c->nlb, F,
                                            c->greedy_cap ? c->greedy_cap : wave_cap, -1,
-                                           c->flags.as<uint32_t>(), s));
+                                           B.flags->as<uint32_t>(), s));
     else
-        HIP_TRY(launch_bucket_flags(c->cell_base.as<uint64_t>(), c->cell_total.as<uint64_t>(), c->nlb, F, cap / 4,
-                                    cap - cap / 4, c->flags.as<uint32_t>(), s));
-    HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), ncell_all,
-                                     c->flag_scan.as<uint64_t>() + ncell_all, c->ws, s));
+        HIP_TRY(launch_bucket_flags(cell_base, cell_total, c->nlb, F, cap / 4, cap - cap / 4, B.flags->as<uint32_t>(), s));
+    HIP_TRY(scan_excl_sum_u32_to_u64(B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), ncell_all,
+                                     B.flag_scan->as<uint64_t>() + ncell_all, c->ws, s));
     uint64_t nbuckets = 0;
-    HIP_TRY(hipMemcpyAsync(&nbuckets, c->flag_scan.as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&nbuckets, B.flag_scan->as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     htrace("sorted: nbuckets read");
-    FK_TRY(ensure(c->buckets, nbuckets * sizeof(Bucket)));
+    FK_TRY(ensure(*B.buckets, nbuckets * sizeof(Bucket)));
     FK_TRY(ensure(okb, total_kmers * 8 * c->KW));
-    FK_TRY(ensure(c->out_counts, total_kmers * 4));
-    FK_TRY(ensure(c->bucket_unique, (nbuckets + 1) * 8));
-    FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
-    HIP_TRY(launch_bucket_write(c->cell_base.as<uint64_t>(), c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(),
-                                c->nlb, F, nbuckets, total_kmers, c->buckets.as<Bucket>(), s));
+    FK_TRY(ensure(*B.out_counts, total_kmers * 4));
+    FK_TRY(ensure(*B.bucket_unique, (nbuckets + 1) * 8));
+    HIP_TRY(launch_bucket_write(cell_base, B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), c->nlb, F, nbuckets,
+                                total_kmers, B.buckets->as<Bucket>(), s));
     BucketSrc src = src_in;
     if (src.np > 0 && c->st_starts) {  // the staged pieces' starts per bucket, read by the wave tier
-        FK_TRY(ensure(c->piece_starts, nbuckets * sizeof(PieceStarts)));
-        HIP_TRY(launch_bucket_pieces(src, c->buckets.as<Bucket>(), nbuckets, c->piece_starts.as<PieceStarts>(), s));
-        src.starts = c->piece_starts.as<PieceStarts>();
+        FK_TRY(ensure(*B.piece_starts, nbuckets * sizeof(PieceStarts)));
+        HIP_TRY(launch_bucket_pieces(src, B.buckets->as<Bucket>(), nbuckets, B.piece_starts->as<PieceStarts>(), s));
+        src.starts = B.piece_starts->as<PieceStarts>();
     }
     // 5: exact count per bucket in LDS; buckets that do not fit take the streaming path
     const uint32_t small_limit = c->force_large ? 0u : cap;
@@ -1621,10 +1656,10 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     c->stats.buckets = nbuckets;
     c->stats.fine_bits = (uint64_t)F;
     if (tiered) {
-        FK_TRY(ensure(c->tier_list, nbuckets * 8));
-        uint32_t *lists = c->tier_list.as<uint32_t>();
-        HIP_TRY(launch_bucket_tiers(c->buckets.as<Bucket>(), nbuckets, wave_cap, cap,
-                                    c->bucket_unique.as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
+        FK_TRY(ensure(*B.tier_list, nbuckets * 8));
+        uint32_t *lists = B.tier_list->as<uint32_t>();
+        HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, cap,
+                                    B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
         // the tier sizes go to pinned memory right behind the tier kernel: the host waits for that
         // copy, not for the wave tier queued after it, before it queues the block tiers
         if (c->pin_tier.ensure(16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
@@ -1632,57 +1667,57 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         HIP_TRY(hipEventRecord(c->tier_ev, s));
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
-            HIP_TRY(launch_bucket_count64_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
-                                               okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                               c->bucket_unique.as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
+            HIP_TRY(launch_bucket_count64_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
+                                               okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                               B.bucket_unique->as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
                                                nullptr, s));
         else
-            HIP_TRY(launch_bucket_count128_wave(src, c->buckets.as<Bucket>(), nbuckets, k,
-                                                okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                                c->bucket_unique.as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
+            HIP_TRY(launch_bucket_count128_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
+                                                okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                B.bucket_unique->as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
                                                 s));
         HIP_TRY(hipEventSynchronize(c->tier_ev));
         uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
         htrace("sorted: tiers read");
         if (ntier[0] && c->KW == 1)
-            HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), ntier[0], k,
-                                          okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                          c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
+            HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k,
+                                          okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                          B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
                                           cap, 99, lists, s));
         else if (ntier[0])
-            HIP_TRY(launch_bucket_sort(2, src, c->buckets.as<Bucket>(), ntier[0], k,
-                                       okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                       c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
+            HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), ntier[0], k,
+                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                       B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, s));
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
             // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
-            HIP_TRY(launch_bucket_count64_big(src, c->buckets.as<Bucket>(), ntier[1], k,
-                                              okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                              c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
+            HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), ntier[1], k,
+                                              okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                              B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
                                               lists + nbuckets, s));
             HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
         }
         if (nlarge) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            HIP_TRY(launch_bucket_sort_large(c->KW, src, c->buckets.as<Bucket>(), ntier[1], k,
+            HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
-                                             c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
+                                             B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
                                              lists + nbuckets, s));
         }
         c->stats.oversize_buckets = nlarge;
     } else {
         if (src.np > 0) return set_err(FK_E_INVALID, "staged pieces need the tiered count");
         if (c->KW == 1)
-            HIP_TRY(launch_bucket_count64(src, c->buckets.as<Bucket>(), nbuckets, k,
-                                          okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                          c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
+            HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nbuckets, k,
+                                          okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                          B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>(),
                                           small_limit, c->dbg_phase, nullptr, s));
         else
-            HIP_TRY(launch_bucket_sort(c->KW, src, c->buckets.as<Bucket>(), nbuckets, k,
-                                       okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                       c->bucket_unique.as<uint64_t>(), c->misc.as<unsigned long long>(),
+            HIP_TRY(launch_bucket_sort(c->KW, src, B.buckets->as<Bucket>(), nbuckets, k,
+                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                       B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>(),
                                        small_limit, nullptr, s));
         uint64_t oversize = 0;
         HIP_TRY(hipMemcpyAsync(&oversize, c->misc.p, 8, hipMemcpyDeviceToHost, s));
@@ -1690,25 +1725,36 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         c->stats.oversize_buckets = oversize;
         if (oversize) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            HIP_TRY(launch_bucket_sort_large(c->KW, src, c->buckets.as<Bucket>(), nbuckets, k,
+            HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), nbuckets, k,
                                              c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
-                                             c->out_counts.as<uint32_t>(), c->bucket_unique.as<uint64_t>(),
+                                             B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
                                              nullptr, s));
         }
     }
-    HIP_TRY(scan_excl_sum_u64(c->bucket_unique.as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
+    *nb_out = nbuckets;
+    return FK_OK;
+}
+
+// The count's result from its buckets: dense_off = the exclusive scan of the distinct keys per bucket,
+// bin_off per local bin (`flag_scan` of the bucket cut: a bin's first cell starts a bucket); kept
+// bucket-major unless want_dense (then compacted into dense_keys / dense_counts).
+static int sorted_result(fk_ctx *c, int F, uint64_t nbuckets, uint64_t total_kmers, DevBuf &okb, CountBufs B) {
+    hipStream_t s = c->stream;
+    FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
+    HIP_TRY(scan_excl_sum_u64(B.bucket_unique->as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
     FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
     c->distinct_pending = true;
     if (!c->want_dense) {
         // the result stays bucket-major (no compaction pass): the buckets' outputs are the result
-        HIP_TRY(launch_bin_offsets(c->flag_scan.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
+        HIP_TRY(launch_bin_offsets(B.flag_scan->as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
                                    c->bin_off.as<uint64_t>(), s));
         c->gapped = true;
         c->dense_ready = false;
         c->res_keys = okb.as<uint64_t>();
         c->res_nbuckets = nbuckets;
         c->res_F = F;
+        c->res_fs = B.flag_scan->as<uint64_t>();
         return FK_OK;
     }
     c->gapped = false;
@@ -1737,12 +1783,23 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
         FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
         FK_TRY(ensure(c->dense_counts, distinct * 4));
     }
-    HIP_TRY(launch_bucket_compact(c->KW, okb.as<uint64_t>(), c->out_counts.as<uint32_t>(),
-                                  c->buckets.as<Bucket>(), nbuckets, c->dense_off.as<uint64_t>(),
+    HIP_TRY(launch_bucket_compact(c->KW, okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                  B.buckets->as<Bucket>(), nbuckets, c->dense_off.as<uint64_t>(),
                                   c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(), s));
-    HIP_TRY(launch_bin_offsets(c->flag_scan.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
+    HIP_TRY(launch_bin_offsets(B.flag_scan->as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
                                c->bin_off.as<uint64_t>(), s));
     return FK_OK;
+}
+
+static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in, uint64_t total_kmers) {
+    // the one-array count writes its buckets' results over the first expansion level (`mid` is dead
+    // once level 2 has run, stream order): one k-mer array less on the device (57 GB at configs[3]'s
+    // per-GPU load, 128-bit keys)
+    DevBuf &okb = (src_in.np == 0 && pl.two_level && c->mid.bytes >= total_kmers * 8 * c->KW) ? c->mid : c->out_keys;
+    uint64_t nb = 0;
+    FK_TRY(sorted_count_buckets(c, pl, src_in, total_kmers, c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(),
+                                main_bufs(c), okb, &nb));
+    return sorted_result(c, pl.F, nb, total_kmers, okb, main_bufs(c));
 }
 
 // After the bin offsets are on the host: the sorted count's distinct total is their last entry.
@@ -2186,6 +2243,8 @@ FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, c
 // ---------------------------------------------------------------------------
 
 static void pieces_reset(fk_ctx *c) {
+    c->pre_done = false;
+    c->pre_np = 0;
     c->npieces = 0;
     c->st_np = 0;
     c->st_kmers = 0;
@@ -2391,6 +2450,120 @@ static int staged_expand(fk_ctx *c, const RecSrc &src, double frac) {
     return staged_expand_chunks(c, (uint32_t)chunks.size(), bkm, frac);
 }
 
+// Pre-count (one rank, k <= 32): worth it when the input is redundant -- the final count then
+// merges the pre-counted distinct keys (far fewer than the k-mers they stand for) with the last
+// pieces' k-mers.  Without redundancy the pre-counted entries are nearly as many as the k-mers and
+// the pre-count is extra work.
+static bool precount_ok(const fk_ctx *c) {
+    if (c->precount == 0 || c->KW != 1 || !staged_eligible(c)) return false;
+    return c->precount == 1 || (c->job_ratio >= 0.0 && c->job_ratio < 0.4);
+}
+
+// The buckets of the pieces expanded so far, counted while later pieces land: a bucket cut over
+// their summed cell totals (pre_total), each bucket's distinct keys ascending with counts at its
+// first slot of pre_keys / pre_counts (bucket-major), pre_unique per bucket.
+static int staged_precount(fk_ctx *c) {
+    hipStream_t s = c->stream;
+    const SortedPlan pl = c->st_plan;
+    const uint64_t ncell_all = (uint64_t)c->nlb << pl.F;
+    HIP_TRY(hipEventRecord(c->pre_ev[0], s));
+    FK_TRY(ensure(c->pre_total, ncell_all * 8));
+    FK_TRY(ensure(c->pre_base, (ncell_all + 1) * 8));
+    HIP_TRY(hipMemcpyAsync(c->pre_total.p, c->st_total.p, ncell_all * 8, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(scan_excl_sum_u64(c->pre_total.as<uint64_t>(), c->pre_base.as<uint64_t>(), ncell_all,
+                              c->pre_base.as<uint64_t>() + ncell_all, c->ws, s));
+    BucketSrc src{nullptr, pl.F};
+    src.np = (int)c->st_np;
+    for (uint32_t p = 0; p < c->st_np; ++p) {
+        src.pk[p] = c->st_keys[p].as<uint64_t>();
+        src.pcb[p] = c->st_cb[p].as<uint64_t>();
+    }
+    CountBufs B{&c->pre_flags, &c->pre_flag_scan, &c->pre_buckets, &c->pre_unique, &c->pre_tier_list,
+                &c->pre_piece_starts, &c->pre_counts};
+    uint64_t nb = 0;
+    FK_TRY(sorted_count_buckets(c, pl, src, c->st_kmers, c->pre_total.as<uint64_t>(), c->pre_base.as<uint64_t>(), B,
+                                c->pre_keys, &nb));
+    HIP_TRY(hipEventRecord(c->pre_ev[1], s));
+    c->pre_nb = nb;
+    c->pre_np = c->st_np;
+    c->pre_kmers = c->st_kmers;
+    c->pre_done = true;
+    htrace("staged: pre-count queued");
+    return FK_OK;
+}
+
+// The final count of a pre-counted job: the pre-count's bucket cut over the job's cells (B2); a
+// bucket whose pre-counted entries plus the later pieces' keys fit a wave is counted from them
+// (k_bucket_merge64_wave), the others from every piece's raw keys by the usual tiers.
+static int staged_count_merge(fk_ctx *c, const SortedPlan &pl) {
+    hipStream_t s = c->stream;
+    const int k = c->cfg.k;
+    const uint64_t nb = c->pre_nb, total = c->st_kmers;
+    FK_TRY(ensure(c->buckets, nb * sizeof(Bucket) + 16));
+    FK_TRY(ensure(c->out_keys, total * 8));
+    FK_TRY(ensure(c->out_counts, total * 4));
+    FK_TRY(ensure(c->bucket_unique, (nb + 1) * 8));
+    FK_TRY(ensure(c->tier_list, nb * 16 + 16));
+    FK_TRY(ensure(c->misc, 64));
+    HIP_TRY(launch_bucket_write(c->cell_base.as<uint64_t>(), c->pre_flags.as<uint32_t>(), c->pre_flag_scan.as<uint64_t>(),
+                                c->nlb, pl.F, nb, total, c->buckets.as<Bucket>(), s));
+    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
+    uint32_t *lists = c->tier_list.as<uint32_t>();
+    HIP_TRY(launch_bucket_tiers_merge(c->pre_buckets.as<Bucket>(), c->pre_unique.as<uint64_t>(), c->buckets.as<Bucket>(),
+                                      nb, pl.wave_cap, pl.cap, c->bucket_unique.as<uint64_t>(), lists,
+                                      c->misc.as<unsigned int>(), s));
+    if (c->pin_tier.ensure(16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t nt[4];
+    memcpy(nt, c->pin_tier.p, 16);
+    htrace("staged: merge tiers read");
+    BucketSrc last{nullptr, pl.F}, all{nullptr, pl.F};
+    last.np = (int)(c->st_np - c->pre_np);
+    all.np = (int)c->st_np;
+    for (uint32_t p = 0; p < c->st_np; ++p) {
+        all.pk[p] = c->st_keys[p].as<uint64_t>();
+        all.pcb[p] = c->st_cb[p].as<uint64_t>();
+        if (p >= c->pre_np) {
+            last.pk[p - c->pre_np] = all.pk[p];
+            last.pcb[p - c->pre_np] = all.pcb[p];
+        }
+    }
+    uint64_t *ok = c->out_keys.as<uint64_t>(), *bu = c->bucket_unique.as<uint64_t>();
+    uint32_t *oc = c->out_counts.as<uint32_t>();
+    const Bucket *b2 = c->buckets.as<Bucket>();
+    if (nt[0]) {
+        if (last.np < 1) return set_err(FK_E_STATE, "pre-counted buckets without later pieces");
+        HIP_TRY(launch_bucket_merge64_wave(c->pre_keys.as<uint64_t>(), c->pre_counts.as<uint32_t>(),
+                                           c->pre_buckets.as<Bucket>(), c->pre_unique.as<uint64_t>(), last, b2, lists,
+                                           nt[0], k, ok, oc, bu, s));
+    }
+    if (nt[1])
+        HIP_TRY(launch_bucket_count64_wave(all, b2, nt[1], k, ok, oc, bu, c->wave_bpw, c->wave_cap, c->wave_slots,
+                                           lists + nb, s));
+    if (nt[2])
+        HIP_TRY(launch_bucket_count64(all, b2, nt[2], k, ok, oc, bu, c->misc.as<unsigned long long>() + 3, pl.cap, 99,
+                                      lists + 2 * nb, s));
+    uint64_t nlarge = 0;
+    if (nt[3]) {
+        HIP_TRY(launch_bucket_count64_big(all, b2, nt[3], k, ok, oc, bu, c->misc.as<unsigned long long>() + 2,
+                                          lists + 3 * nb, s));
+        HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (nlarge) {
+            FK_TRY(ensure(c->scratch, total * 8));
+            HIP_TRY(launch_bucket_sort_large(1, all, b2, nt[3], k, c->scratch.as<uint64_t>(), ok, oc, bu,
+                                             lists + 3 * nb, s));
+        }
+    }
+    c->stats.buckets = nb;
+    c->stats.fine_bits = (uint64_t)pl.F;
+    c->stats.oversize_buckets = nlarge;
+    CountBufs B{&c->pre_flags, &c->pre_flag_scan, &c->buckets, &c->bucket_unique, &c->tier_list, &c->piece_starts,
+                &c->out_counts};
+    return sorted_result(c, pl.F, nb, total, c->out_keys, B);
+}
+
 // The job's count over the staged pieces: buckets over the summed cell totals, each bucket's keys
 // read from every piece (BucketSrc pieces), the dense result and its bin offsets.
 static int staged_count(fk_ctx *c) {
@@ -2404,13 +2577,17 @@ static int staged_count(fk_ctx *c) {
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
                               c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
-    BucketSrc src{nullptr, pl.F};
-    src.np = (int)c->st_np;
-    for (uint32_t p = 0; p < c->st_np; ++p) {
-        src.pk[p] = c->st_keys[p].as<uint64_t>();
-        src.pcb[p] = c->st_cb[p].as<uint64_t>();
+    if (c->pre_done && c->st_np > c->pre_np) {
+        FK_TRY(staged_count_merge(c, pl));
+    } else {
+        BucketSrc src{nullptr, pl.F};
+        src.np = (int)c->st_np;
+        for (uint32_t p = 0; p < c->st_np; ++p) {
+            src.pk[p] = c->st_keys[p].as<uint64_t>();
+            src.pcb[p] = c->st_cb[p].as<uint64_t>();
+        }
+        FK_TRY(sorted_count(c, pl, src, c->st_kmers));
     }
-    FK_TRY(sorted_count(c, pl, src, c->st_kmers));
     HIP_TRY(hipEventRecord(c->ev[7], s));
     c->h_bin_off.assign((size_t)nlb + 1, 0);
     if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
@@ -2425,7 +2602,8 @@ static int staged_count(fk_ctx *c) {
         mx += ev_ms(c->st_ev[4 * p + 2], c->st_ev[4 * p + 3]);
     }
     c->stats.ms_partition = mp;
-    c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]);
+    c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]) + (c->pre_done ? ev_ms(c->pre_ev[0], c->pre_ev[1]) : 0.0);
+    c->stats.precounted = c->pre_done ? 1u : 0u;
     c->stats.ms_merge = 0.0;
     c->stats.pieces_counted = c->st_np;
     c->stats.records_received = c->nrec;
@@ -2481,6 +2659,7 @@ static int local_maybe_piece(fk_ctx *c) {
         FK_TRY(staged_expand(c, src, c->job_bytes ? (double)(nt * fm_tile_bytes(c->fused_nt)) / (double)c->job_bytes
                                                   : 0.0));
         if (c->st_np > np0) c->npieces += 1;  // (a piece without k-mers adds none)
+        if (!c->pre_done && c->st_np == c->pre_at && precount_ok(c)) FK_TRY(staged_precount(c));
         return FK_OK;
     }
     return count_piece(c, [&] { return reduce_src(c, src); }, false);
@@ -3093,7 +3272,7 @@ static int materialize_dense(fk_ctx *c) {
 static int gather_bin(fk_ctx *c, uint32_t lb, uint64_t *dkeys, uint32_t *dcounts) {
     hipStream_t s = c->stream;
     uint64_t q[2] = {0, c->res_nbuckets};
-    const uint64_t *fs = c->flag_scan.as<uint64_t>();
+    const uint64_t *fs = c->res_fs;
     HIP_TRY(hipMemcpyAsync(&q[0], fs + ((uint64_t)lb << c->res_F), 8, hipMemcpyDeviceToHost, s));
     if (lb + 1 < c->nlb) HIP_TRY(hipMemcpyAsync(&q[1], fs + ((uint64_t)(lb + 1) << c->res_F), 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -213,6 +213,17 @@ hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave
 hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique, int bpw,
                                       uint32_t wave_cap, uint32_t wave_slots, const uint32_t *list, hipStream_t s);
+// final count of a pre-counted staged job (k <= 32): tiers of the final buckets b2 (the cells of the
+// pre-count's buckets b1 over the whole job) and the wave kernel that counts a bucket from the
+// pre-counted entries (r1 at b1[q].begin, u1[q] of them, weights = their counts) plus the raw keys
+// of the later pieces (`last`, a staged-piece view)
+hipError_t launch_bucket_tiers_merge(const Bucket *b1, const uint64_t *u1, const Bucket *b2, uint64_t nb,
+                                     uint32_t wave_cap, uint32_t block_cap, uint64_t *bucket_unique, uint32_t *lists,
+                                     unsigned int *counts, hipStream_t s);
+hipError_t launch_bucket_merge64_wave(const uint64_t *r1_keys, const uint32_t *r1_counts, const Bucket *b1,
+                                      const uint64_t *u1, const BucketSrc &last, const Bucket *b2,
+                                      const uint32_t *list, uint64_t nlist, int k, uint64_t *out_keys,
+                                      uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s);
 // staged pieces (src.np > 0) in the wave tier: the default tier configuration only
 bool wave_staged_supported(uint32_t wave_cap, uint32_t wave_slots, int bpw);
 // staged pieces in the 128-bit wave tier: the default table size only

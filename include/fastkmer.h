@@ -85,6 +85,8 @@ typedef struct fk_stats {
     /* pieces counted while later ones were still being copied in / received (sorted count) */
     uint64_t pieces_counted;   /* piece results merged by the last fk_finish (0: one count of the whole input) */
     double ms_merge;           /* their k-way merge (k_merge_plan / k_merge_segments / k_merge_compact) */
+    uint64_t precounted;       /* 1: the job's first staged pieces were counted while the rest landed, the final
+                                  count merged them with the later pieces' k-mers */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

@@ -9,6 +9,7 @@ devices driven alternately from one thread.
 """
 import concurrent.futures as cf
 
+import numpy as np
 import pytest
 import torch
 
@@ -87,17 +88,19 @@ def test_device_input_then_host_input_on_one_context():
         assert_same_as_oracle(kc, ref)
 
 
-def test_bin_owners_rejected_with_grouped_emit():
-    # fk_set_bin_owners after fk_set_grouped_emit: the emitted layout would not match the counts
-    # handed to the all-to-all, so the call fails (FK_E_STATE) and the context stays usable
+def test_bin_owners_with_grouped_emit():
+    # fk_set_bin_owners with the grouped emit (the library's exchange layout): the (owner, local bin)
+    # parts follow the new owners after a new fk_map, and the records per destination equal the
+    # plain emit's under the same owners
     fasta = _fasta(25)
+    owner = [(b + 1) % 2 for b in range(2048)]  # not the default bin % 2
+    with fk.KmerCounter(28, 10, 3, 2048, False, 0, n_ranks=2, rank=0) as kc:
+        kc.ingest(fasta)
+        kc.map()
+        plain = kc.set_bin_owners(owner)
     with fk.KmerCounter(28, 10, 3, 2048, False, 0, n_ranks=2, rank=0) as kc:
         kc.ingest(fasta)
         kc.set_grouped_emit(True)
-        kc.map()
-        with pytest.raises(fk.FastKmerError):
-            kc.set_bin_owners([b % 2 for b in range(2048)])
-        kc.set_grouped_emit(False)  # toggling the emit layout asks for a new fk_map
-        kc.map()
-        counts = kc.set_bin_owners([(b + 1) % 2 for b in range(2048)])
-        assert len(counts) == 2 and sum(counts) > 0
+        kc.set_bin_owners(owner)
+        assert np.array_equal(kc.bin_owners(), owner)
+        assert kc.map() == plain and sum(plain) > 0

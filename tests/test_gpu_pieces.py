@@ -26,11 +26,14 @@ from test_gpu_parity import assert_same_as_oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 0], ids=["staged", "merge"])
+@pytest.fixture(params=[1, 0, 2], ids=["staged", "merge", "staged-precount"])
 def small_pieces(monkeypatch, request):
+    # 2: staged with the pre-count forced (FASTKMER_PRECOUNT=1): the first two pieces' buckets are
+    # counted while the rest lands, the final count merges them with the later pieces' k-mers
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
-    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(request.param))
+    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(min(request.param, 1)))
+    monkeypatch.setenv("FASTKMER_PRECOUNT", "1" if request.param == 2 else "0")
     return request.param
 
 
@@ -52,6 +55,7 @@ def test_piece_counts_merge_vs_oracle(small_pieces, k, m, read_len, B):
     kc = count_pinned(fasta, k, m, B, repeat=2)  # twice: the piece buffers are reused by the second job
     st = kc.stats()
     assert st["pieces_counted"] >= 4 and st["fused_map"] == 1
+    assert st["precounted"] == (1 if small_pieces == 2 and k <= 32 else 0)
     ref = oracle.OracleResult(fasta, k, m, B)
     assert st["kmers"] == ref.total_kmers and st["distinct"] == ref.distinct
     assert_same_as_oracle(kc, ref)
@@ -130,9 +134,10 @@ def test_piece_counts_many_small_pieces(monkeypatch, mode):
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
 
 
-@pytest.mark.parametrize("cuts,one_level,chunks", [("0.45,0.7,0.85", "0.2", 0), ("0.3", "0", 0),
-                                                   ("0.2,0.25,0.97", "0.5", 0), ("0.45,0.7,0.85", "0.2", 7)])
-def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks):
+@pytest.mark.parametrize("cuts,one_level,chunks,pre", [("0.45,0.7,0.85", "0.2", 0, "0"), ("0.3", "0", 0, "0"),
+                                                       ("0.2,0.25,0.97", "0.5", 0, "0"), ("0.45,0.7,0.85", "0.2", 7, "0"),
+                                                       ("0.45,0.7,0.85", "0", 0, "1"), ("0.45,0.7,0.85", "0", 7, "1")])
+def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks, pre):
     # a 1 GB job in one fk_ingest call (pinned): staged pieces at the job-size cuts (the
     # bench's path) against the same job counted whole on the device (FASTKMER_PIECE_COUNT=0),
     # every bin's keys and counts equal; a sampled slice of bins against the oracle is in
@@ -147,6 +152,7 @@ def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks):
     torch.cuda.synchronize()
     monkeypatch.setenv("FASTKMER_PIECE_CUTS", cuts)
     monkeypatch.setenv("FASTKMER_STAGED_ONE_LEVEL", one_level)  # pieces below this job fraction: one pass
+    monkeypatch.setenv("FASTKMER_PRECOUNT", pre)  # 1: the first two pieces counted while the rest lands
     a = fk.KmerCounter(28, 10, 3, 2048)
     if chunks:  # a streamed job: fk_ingest_reserve announces its size, the cuts follow it
         a.reserve(host.numel())
@@ -158,6 +164,7 @@ def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks):
     a.finish()
     st = a.stats()
     assert st["pieces_counted"] == cuts.count(",") + 2
+    assert st["precounted"] == int(pre)
     monkeypatch.setenv("FASTKMER_PIECE_COUNT", "0")
     b = fk.KmerCounter(28, 10, 3, 2048)
     b.ingest_device(dev.data_ptr(), dev.numel())
