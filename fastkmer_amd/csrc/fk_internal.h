@@ -230,9 +230,17 @@ bool wave_staged_supported(uint32_t wave_cap, uint32_t wave_slots, int bpw);
 bool wave128_staged_supported(uint32_t wave_slots);
 // dst[i] += src[i] (dst = src when `copy`)
 hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
+// skip_le: listed buckets of at most this many keys were counted by a wave tier (skipped)
 hipError_t launch_bucket_sort(int KW, const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                               uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                              unsigned long long *oversize, uint32_t small_limit, const uint32_t *list, hipStream_t s);
+                              unsigned long long *oversize, uint32_t small_limit, const uint32_t *list, hipStream_t s,
+                              uint32_t skip_le = 0);
+// 128-bit keys, the listed buckets of WAVE128_BUCKET_CAP < n <= WAVE128_MID_CAP keys: one wave each,
+// a 768-slot table (the others on the list are skipped)
+constexpr uint32_t WAVE128_MID_CAP = 512;
+hipError_t launch_bucket_count128_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
+                                           uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
+                                           uint64_t *bucket_unique, hipStream_t s);
 hipError_t launch_bucket_sort_large(int KW, const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                     uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
                                     uint64_t *bucket_unique, const uint32_t *list, hipStream_t s);

@@ -87,6 +87,7 @@ typedef struct fk_stats {
     double ms_merge;           /* their k-way merge (k_merge_plan / k_merge_segments / k_merge_compact) */
     uint64_t precounted;       /* 1: the job's first staged pieces were counted while the rest landed, the final
                                   count merged them with the later pieces' k-mers */
+    uint64_t block_buckets;    /* buckets above the wave tier (the block / big tiers and the large path) */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
