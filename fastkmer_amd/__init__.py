@@ -142,6 +142,7 @@ def lib():
         "fk_balance_bins": (ctypes.c_int, [P, ctypes.c_char_p, SZ]),
         "fk_balance_bins_file": (ctypes.c_int, [P, ctypes.c_char_p, I32, I32, ctypes.c_double]),
         "fk_exchange_plan": (ctypes.c_int, [I32, I32, P, P, U64, P, P, P, P, P]),
+        "fk_debug_map_cycles": (ctypes.c_int, [P, I32]),
         "fk_debug_wave_count": (ctypes.c_int, [I32, I32, I32, ctypes.c_uint32, ctypes.c_uint32, I32, P,
                                                ctypes.c_uint32, P, P, P]),
     }

@@ -3376,6 +3376,19 @@ FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t
     return rc;
 }
 
+// measurement hook (a library built with -DFK_PROBES; FK_E_STATE otherwise): the fused map's
+// per-phase wave cycles (s_memtime) summed over every launch since the last reset
+FK_EXPORT int fk_debug_map_cycles(uint64_t *out16, int32_t reset) {
+    if (!out16) return set_err(FK_E_INVALID, "null argument");
+    const hipError_t e = map_fused_cycles(reinterpret_cast<unsigned long long *>(out16), reset != 0);
+    if (e == hipErrorNotSupported) {
+        (void)hipGetLastError();
+        return set_err(FK_E_STATE, "phase stamps exist only in a library built with -DFK_PROBES");
+    }
+    HIP_TRY(e);
+    return FK_OK;
+}
+
 FK_EXPORT int fk_get_stats(fk_ctx *c, fk_stats *out) {
     if (!c || !out) return set_err(FK_E_INVALID, "null argument");
     *out = c->stats;

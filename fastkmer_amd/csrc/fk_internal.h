@@ -103,6 +103,8 @@ bool map_fused_supported(int k, int m, uint32_t nbins);
 uint64_t fm_tile_bytes(int nth);
 uint64_t fm_span_bytes(int nth);
 uint32_t map_fused_tcap();
+// measurement build (-DFK_PROBES): the fused map's per-phase wave cycles summed since the last reset
+hipError_t map_fused_cycles(unsigned long long *out16, bool reset);
 uint32_t map_fused_cslot();
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
                             uint64_t ntiles, FastMod fm, uint32_t *hdrs, uint16_t *pos, uint32_t *codes,

@@ -279,6 +279,11 @@ int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t c0, uint3
                         const uint64_t *keys, uint32_t n, uint64_t *out_keys, uint32_t *out_counts,
                         uint32_t *n_out);
 
+/* Measurement hook: per-phase wave cycles of the fused map kernel summed over
+ * its launches since the last reset (out[0..16)); only a library built with
+ * -DFK_PROBES records them (FK_E_STATE otherwise). */
+int fk_debug_map_cycles(uint64_t *out16, int32_t reset);
+
 /* ---- bin-signature diagnostics (executeFindBinSignaturesJob, SBKC:956-986) ----
  * fk_signature_counts: after the final fk_ingest (the input is left in place,
  *   fk_map may follow), d_counts[v] (device memory of the ctx device, uint64)
