@@ -154,8 +154,21 @@ def build_jni(force: bool = False) -> str | None:
     return JNI_LIB
 
 
+def build_variant(name: str, defs: list[str], force: bool = False) -> str:
+    """An A/B build of the library with extra -D flags into fastkmer_amd/lib_<name>/ (measurement
+    only: scripts select it with FASTKMER_LIB)."""
+    lib = os.path.join(PKG, f"lib_{name}", "libfastkmer.so")
+    deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "fastkmer.h")]
+    _build_lib(lib, deps, force, defs)
+    return lib
+
+
 if __name__ == "__main__":
     if "--probes" in sys.argv:
         build_probes(force="--force" in sys.argv)
+    elif "--variant" in sys.argv:  # python -m fastkmer_amd.build --variant NAME -DX=1 ...
+        i = sys.argv.index("--variant")
+        build_variant(sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")],
+                      force="--force" in sys.argv)
     else:
         build(force="--force" in sys.argv)
