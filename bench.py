@@ -349,7 +349,7 @@ def main() -> None:
                           "partition": hs["ms_partition"], "count": hs["ms_count"]},
             "pcie_h2d_GBps": r0.fasta_bytes / (hs["ms_h2d"] * 1e-3) / 1e9 if hs["ms_h2d"] else None,
             "kmers_per_gpu": hs["kmers"], "distinct_rank0": hs["distinct"],
-            "buckets_rank0": {"all": hs["buckets"], "above_wave_tier": hs["block_buckets"],
+            "buckets_rank0": {"all": hs["buckets"], "above_wave_tier": hs["block_buckets"], "above_2048_keys": hs["big_buckets"],
                               "large_path": hs["oversize_buckets"], "cell_bits": hs["fine_bits"]},
         }
         if n_ranks > 1:

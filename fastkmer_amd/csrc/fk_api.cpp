@@ -394,7 +394,7 @@ struct fk_ctx {
     // configs[1]: 23.14 ms per step against 22.97 without -- the final count's cost is per bucket
     // (table clears, ranks), not per key, so merging fewer entries saves little)
     int precount = 0;
-    int mid128 = 1;  // FASTKMER_MID128=0: 128-bit buckets above the wave tier go to the radix sort
+    int mid_tier = 1;  // FASTKMER_MID_TIER=0: buckets above the wave tier go to the block kernels / radix sort
     uint32_t pre_at = 2;
     bool pre_done = false;
     uint32_t pre_np = 0;
@@ -604,7 +604,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
     if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
     if (const char *pc = getenv("FASTKMER_PRECOUNT"); pc && pc[0]) c->precount = atoi(pc);
-    if (const char *m1 = getenv("FASTKMER_MID128"); m1 && m1[0]) c->mid128 = atoi(m1);
+    if (const char *m1 = getenv("FASTKMER_MID_TIER"); m1 && m1[0]) c->mid_tier = atoi(m1);
     if (const char *pa = getenv("FASTKMER_PRECOUNT_AT"); pa && pa[0])
         c->pre_at = (uint32_t)std::max(1, std::min(STAGE_MAXP - 1, atoi(pa)));
     if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
@@ -1684,23 +1684,30 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
         htrace("sorted: tiers read");
         c->stats.block_buckets = ntier[0];
-        if (ntier[0] && c->KW == 1)
+        c->stats.big_buckets = ntier[1];
+        if (ntier[0] && c->KW == 1) {
+            // the block-tier buckets of at most WAVE_MID_CAP keys take a wave with a 1536-slot table
+            // (minimizer-prefix cells of large bins), the rest the block kernel
+            if (c->mid_tier)
+                HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                       B.bucket_unique->as<uint64_t>(), s));
             HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k,
                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                           B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
-                                          cap, 99, lists, s));
-        else if (ntier[0]) {
+                                          cap, 99, lists, s, c->mid_tier ? WAVE_MID_CAP : 0u));
+        } else if (ntier[0]) {
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
             // 768-slot table (a cell of a large bin, ~340 keys at configs[3]'s per-GPU bins), the rest
             // the LDS radix sort
-            if (c->mid128)
+            if (c->mid_tier)
                 HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                         okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                                         B.bucket_unique->as<uint64_t>(), s));
             HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), ntier[0], k,
                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                        B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
-                                       lists, s, c->mid128 ? WAVE128_MID_CAP : 0u));
+                                       lists, s, c->mid_tier ? WAVE128_MID_CAP : 0u));
         }
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {

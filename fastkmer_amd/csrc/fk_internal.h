@@ -184,11 +184,16 @@ hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags,
 hipError_t launch_bucket_count64(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
-                                 const uint32_t *list, hipStream_t s);
+                                 const uint32_t *list, hipStream_t s, uint32_t mid_cap = 0);
 hipError_t launch_bucket_count64_big(const BucketSrc &src, const Bucket *buckets, uint64_t nlist, int k,
                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                      unsigned long long *oversize, const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
+// k <= 32: the listed buckets of WAVE_BUCKET_CAP < n <= WAVE_MID_CAP keys, one wave each
+constexpr uint32_t WAVE_MID_CAP = 1024;
+hipError_t launch_bucket_count64_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
+                                          uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
+                                          uint64_t *bucket_unique, hipStream_t s);
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,

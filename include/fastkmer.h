@@ -87,7 +87,8 @@ typedef struct fk_stats {
     double ms_merge;           /* their k-way merge (k_merge_plan / k_merge_segments / k_merge_compact) */
     uint64_t precounted;       /* 1: the job's first staged pieces were counted while the rest landed, the final
                                   count merged them with the later pieces' k-mers */
-    uint64_t block_buckets;    /* buckets above the wave tier (the block / big tiers and the large path) */
+    uint64_t block_buckets;    /* buckets above the wave tier of at most 2048 keys (mid wave tier, block kernel) */
+    uint64_t big_buckets;      /* buckets above 2048 keys (the big-table kernel, then the large path) */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

@@ -19,5 +19,12 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_
 done
 python3 "$R/scripts/pmc_kernels.py" "$O" map_fused > $O/pmc_map.txt 2>&1; cat $O/pmc_map.txt
 cd $R
-[ -n "$C3" ] && { timeout -k 10 300 python -u bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline > $O/c3.json 2> $O/c3.err || { tail -20 $O/c3.err; exit 1; }; cat $O/c3.json; }
-true
+if [ -n "$C3" ]; then
+  timeout -k 10 300 python -u bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline > $O/c3.json 2> $O/c3.err || { tail -20 $O/c3.err; exit 1; }; cat $O/c3.json
+  for pa in 2 3; do
+    FASTKMER_PRECOUNT=1 FASTKMER_PRECOUNT_AT=$pa timeout -k 10 300 python -u bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline > $O/c3_pre$pa.json 2> $O/c3_pre$pa.err || { tail -20 $O/c3_pre$pa.err; exit 1; }; cat $O/c3_pre$pa.json
+  done
+fi
+cd /tmp
+FK_MAP_REPS=3 timeout -s KILL 90 rocprofv3 --pmc SQ_IFETCH SQC_ICACHE_HITS SQC_ICACHE_MISSES -d "$O/p9" -o run --output-format csv -- python3 "$R/scripts/map_once.py" > "$O/p9.log" 2>&1 || { echo "icache pass rc=$?"; exit 0; }
+python3 "$R/scripts/pmc_kernels.py" "$O" map_fused > $O/pmc_map.txt 2>&1; cat $O/pmc_map.txt

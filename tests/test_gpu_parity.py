@@ -432,6 +432,23 @@ def test_big_bins_two_level_vs_oracle():
     assert_same_as_oracle(kc, ref)
 
 
+@pytest.mark.parametrize("mid", ["1", "0"])
+def test_mid_tier_buckets_vs_oracle(monkeypatch, mid):
+    # few large bins of a mostly distinct input (~1.4 M k-mers per bin) cut into cells of ~600 keys
+    # (FASTKMER_DEBUG_CELL_TARGET): buckets of 513..2048 keys -- at configs[2]'s per-GPU bins the
+    # cells of the k-mers that start with a frequent minimizer -- counted by the mid wave tier
+    # (<= 1024 keys, FASTKMER_MID_TIER=1) and the block kernel, or by the block kernel alone
+    monkeypatch.setenv("FASTKMER_MID_TIER", mid)
+    monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", "600")
+    fasta = fk.synth_fasta(300_000, 100, 3_000_000_000, seed=71)
+    kc = run_counter(fasta, 28, 10, 3, 16)
+    st = kc.stats()
+    assert st["block_buckets"] > 10_000, st
+    ref = oracle.OracleResult(fasta, 28, 10, 16, threads=4)
+    assert st["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref)
+
+
 @pytest.mark.parametrize("slots", ["768", "1024"])
 @pytest.mark.parametrize("k,m", [(28, 10), (55, 12)])
 def test_wave_tables_of_distinct_keys_vs_oracle(monkeypatch, slots, k, m):
