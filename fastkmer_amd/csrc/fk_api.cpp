@@ -269,6 +269,7 @@ struct fk_ctx {
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
     int fused_probe = 0;       // FASTKMER_FUSED_PROBE: stop the fused map kernel after a phase (timing only)
     int fused_nt = 512;        // FASTKMER_FUSED_NT: threads per fused map workgroup (256 or 512)
+    int split_map = 0;         // FASTKMER_SPLIT_MAP=1: the map as a parse kernel + a signature-pass kernel (measurement)
     bool last_map_fused = false;  // the last fk_map used the fused kernel (stats, tests)
     // grouped emit (fk_set_grouped_emit): send buffer grouped by (destination, local bin)
     bool grouped = false;
@@ -305,6 +306,7 @@ struct fk_ctx {
     DevBuf rec_pos;               // fused map: every record's first position in its tile's code stream (u16)
     DevBuf rec_code;              // fused map: per tile, the tile's 2-bit code stream (map_fused_cslot() words)
     DevBuf tstat;                 // fused map: per tile (k-mers, positions)
+    DevBuf map_vslots;            // split map: the parse kernel's valid streams for the passes (MAP_VSLOT_TILES tiles)
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
@@ -394,7 +396,7 @@ struct fk_ctx {
     // configs[1]: 23.14 ms per step against 22.97 without -- the final count's cost is per bucket
     // (table clears, ranks), not per key, so merging fewer entries saves little)
     int precount = 0;
-    int mid_tier = 1;  // FASTKMER_MID_TIER=0: buckets above the wave tier go to the block kernels / radix sort
+    int mid_tier = 1;  // FASTKMER_MID128=0: 128-bit buckets above the wave tier go to the radix sort
     uint32_t pre_at = 2;
     bool pre_done = false;
     uint32_t pre_np = 0;
@@ -577,6 +579,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 #ifdef FK_PROBES
     const char *fp = getenv("FASTKMER_FUSED_PROBE");
     if (fp && fp[0]) c->fused_probe = atoi(fp);
+    if (const char *sm = getenv("FASTKMER_SPLIT_MAP"); sm && sm[0]) c->split_map = atoi(sm);
     const char *lp = getenv("FASTKMER_LH_PROBE");
     if (lp && lp[0]) c->lh_probe = atoi(lp);
 #endif
@@ -604,7 +607,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
     if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
     if (const char *pc = getenv("FASTKMER_PRECOUNT"); pc && pc[0]) c->precount = atoi(pc);
-    if (const char *m1 = getenv("FASTKMER_MID_TIER"); m1 && m1[0]) c->mid_tier = atoi(m1);
+    if (const char *m1 = getenv("FASTKMER_MID128"); m1 && m1[0]) c->mid_tier = atoi(m1);
     if (const char *pa = getenv("FASTKMER_PRECOUNT_AT"); pa && pa[0])
         c->pre_at = (uint32_t)std::max(1, std::min(STAGE_MAXP - 1, atoi(pa)));
     if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
@@ -678,7 +681,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
-                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat,
+                      &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat, &c->map_vslots,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
                       &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
@@ -795,6 +798,29 @@ static bool premap_eligible(const fk_ctx *c) {
 // lie below `landed`; `final_` = the input ends at `landed` (every remaining
 // tile, the last one sets the record total).  Runs on the map stream after
 // the copy stream's segment event.
+// The map of tiles [t0, t0 + nt) of the input fa[0, n): parse then signature passes in two kernels
+// per MAP_VSLOT_TILES tiles (the parse's waves are latency-bound, the passes' VALU-bound; apart, each
+// kernel's waves keep the SIMDs busy), or the fused kernel (FASTKMER_SPLIT_MAP=0, the 256-thread
+// tiles, probes).  map_vslots is sized by the callers (map_vslots_reserve).
+constexpr uint64_t MAP_VSLOT_TILES = 32768;  // ~1.07 GB of FASTA per split launch pair (140 MB of slots)
+static bool map_split(const fk_ctx *c) { return c->split_map && c->fused_nt == 512 && !c->fused_probe; }
+static int map_vslots_reserve(fk_ctx *c, uint64_t ntiles) {
+    if (!map_split(c)) return FK_OK;
+    return ensure(c->map_vslots, std::min(ntiles, MAP_VSLOT_TILES) * map_fused_vslot() * 4);
+}
+static int map_launch(fk_ctx *c, const uint8_t *fa, uint64_t n, int more, uint64_t t0, uint64_t nt, hipStream_t s) {
+    const uint64_t cap = map_split(c) ? c->map_vslots.bytes / ((uint64_t)map_fused_vslot() * 4) : 0;
+    for (uint64_t b = 0; b < nt;) {
+        const uint64_t m = cap ? std::min(cap, nt - b) : nt - b;
+        HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, fa, n, more, t0 + b, m, c->fm,
+                                 c->rec_hdr.as<uint32_t>(), c->rec_pos.as<uint16_t>(), c->rec_code.as<uint32_t>(),
+                                 c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), c->counters.as<unsigned long long>(),
+                                 s, c->fused_probe, cap ? c->map_vslots.as<uint32_t>() : nullptr));
+        b += m;
+    }
+    return FK_OK;
+}
+
 static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
     const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
     const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
@@ -805,10 +831,7 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
                        (unsigned long long)end);
     hipStream_t s = c->stream;
     if (c->pm_tiles == 0) HIP_TRY(hipEventRecord(c->ev[10], s));
-    HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles,
-                             end - c->pm_tiles, c->fm, c->rec_hdr.as<uint32_t>(), c->rec_pos.as<uint16_t>(),
-                             c->rec_code.as<uint32_t>(), c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(),
-                             c->counters.as<unsigned long long>(), s, c->fused_probe));
+    FK_TRY(map_launch(c, c->d_fasta, landed, final_ ? 0 : 1, c->pm_tiles, end - c->pm_tiles, s));
     c->pm_tiles = end;
     if (final_) HIP_TRY(hipEventRecord(c->ev[11], s));
     return FK_OK;
@@ -872,6 +895,7 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         if (c->rec_hdr.bytes < hdr_need) FK_TRY(grow_keep(c->rec_hdr, hdr_need, c->rec_hdr.bytes, s));
         if (c->rec_pos.bytes < pos_need) FK_TRY(grow_keep(c->rec_pos, pos_need, c->rec_pos.bytes, s));
         if (c->rec_code.bytes < code_need) FK_TRY(grow_keep(c->rec_code, code_need, c->rec_code.bytes, s));
+        FK_TRY(map_vslots_reserve(c, tiles));
         if (fresh) {
             FK_TRY(ensure(c->counters, 64));
             HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
@@ -1151,13 +1175,11 @@ static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     FK_TRY(ensure(c->rec_hdr, ntiles * map_fused_tcap() * 4));
     FK_TRY(ensure(c->rec_pos, ntiles * map_fused_tcap() * 2));
     FK_TRY(ensure(c->rec_code, ntiles * map_fused_cslot() * 4));
+    FK_TRY(map_vslots_reserve(c, ntiles));
     HIP_TRY(hipEventRecord(c->ev[2], s));
     HIP_TRY(hipMemsetAsync(c->counters.p, 0, 64, s));
     HIP_TRY(hipEventRecord(c->ev[10], s));
-    HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, c->d_fasta, n, 0, 0, ntiles, c->fm,
-                             c->rec_hdr.as<uint32_t>(), c->rec_pos.as<uint16_t>(), c->rec_code.as<uint32_t>(),
-                             c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), c->counters.as<unsigned long long>(), s,
-                             c->fused_probe));
+    FK_TRY(map_launch(c, c->d_fasta, n, 0, 0, ntiles, s));
     HIP_TRY(hipEventRecord(c->ev[11], s));
     HIP_TRY(launch_tile_totals(c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), ntiles,
                                c->counters.as<unsigned long long>(), s));
@@ -1686,16 +1708,10 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         c->stats.block_buckets = ntier[0];
         c->stats.big_buckets = ntier[1];
         if (ntier[0] && c->KW == 1) {
-            // the block-tier buckets of at most WAVE_MID_CAP keys take a wave with a 1536-slot table
-            // (minimizer-prefix cells of large bins), the rest the block kernel
-            if (c->mid_tier)
-                HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
-                                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                       B.bucket_unique->as<uint64_t>(), s));
             HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k,
                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                           B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
-                                          cap, 99, lists, s, c->mid_tier ? WAVE_MID_CAP : 0u));
+                                          cap, 99, lists, s));
         } else if (ntier[0]) {
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
             // 768-slot table (a cell of a large bin, ~340 keys at configs[3]'s per-GPU bins), the rest
@@ -1711,7 +1727,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         }
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
-            // buckets of 2049..5888 keys in one workgroup's LDS; larger ones stay REDO
+            // buckets above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
             HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), ntier[1], k,
                                               okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                               B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 2,

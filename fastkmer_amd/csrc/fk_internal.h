@@ -106,10 +106,11 @@ uint32_t map_fused_tcap();
 // measurement build (-DFK_PROBES): the fused map's per-phase wave cycles summed since the last reset
 hipError_t map_fused_cycles(unsigned long long *out16, bool reset);
 uint32_t map_fused_cslot();
+uint32_t map_fused_vslot();  // split map: valid-stream slot words per tile (vslots)
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,
                             uint64_t ntiles, FastMod fm, uint32_t *hdrs, uint16_t *pos, uint32_t *codes,
                             uint32_t *tcnt, uint32_t *tstat, unsigned long long *counters, hipStream_t s,
-                            int probe = 0);
+                            int probe = 0, uint32_t *vslots = nullptr);
 // counters[0] / [1] / [3] = records / k-mers / positions summed over the fused map's tiles [0, ntiles)
 hipError_t launch_tile_totals(const uint32_t *tcnt, const uint32_t *tstat, uint64_t ntiles,
                               unsigned long long *counters, hipStream_t s);
@@ -184,16 +185,11 @@ hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags,
 hipError_t launch_bucket_count64(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
-                                 const uint32_t *list, hipStream_t s, uint32_t mid_cap = 0);
+                                 const uint32_t *list, hipStream_t s);
 hipError_t launch_bucket_count64_big(const BucketSrc &src, const Bucket *buckets, uint64_t nlist, int k,
                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                      unsigned long long *oversize, const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
-// k <= 32: the listed buckets of WAVE_BUCKET_CAP < n <= WAVE_MID_CAP keys, one wave each
-constexpr uint32_t WAVE_MID_CAP = 1024;
-hipError_t launch_bucket_count64_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
-                                          uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
-                                          uint64_t *bucket_unique, hipStream_t s);
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,

@@ -432,18 +432,16 @@ def test_big_bins_two_level_vs_oracle():
     assert_same_as_oracle(kc, ref)
 
 
-@pytest.mark.parametrize("mid", ["1", "0"])
-def test_mid_tier_buckets_vs_oracle(monkeypatch, mid):
-    # few large bins of a mostly distinct input (~1.4 M k-mers per bin) cut into cells of ~600 keys
-    # (FASTKMER_DEBUG_CELL_TARGET): buckets of 513..2048 keys -- at configs[2]'s per-GPU bins the
-    # cells of the k-mers that start with a frequent minimizer -- counted by the mid wave tier
-    # (<= 1024 keys, FASTKMER_MID_TIER=1) and the block kernel, or by the block kernel alone
-    monkeypatch.setenv("FASTKMER_MID_TIER", mid)
-    monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", "600")
+def test_block_and_big_tiers_vs_oracle(monkeypatch):
+    # few large bins of a mostly distinct input (~1.4 M k-mers per bin) cut into cells of up to ~2600 keys
+    # (FASTKMER_DEBUG_CELL_TARGET): buckets of 513..2048 keys (the block kernel) and above (the
+    # 6144-slot big-table kernel, the streaming path past 4096 distinct keys) -- at configs[2]'s
+    # per-GPU bins, the cells of the k-mers that start with a frequent minimizer
+    monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", "2600")
     fasta = fk.synth_fasta(300_000, 100, 3_000_000_000, seed=71)
     kc = run_counter(fasta, 28, 10, 3, 16)
     st = kc.stats()
-    assert st["block_buckets"] > 10_000, st
+    assert st["block_buckets"] > 1000 and st["big_buckets"] > 1000, st
     ref = oracle.OracleResult(fasta, 28, 10, 16, threads=4)
     assert st["kmers"] == ref.total_kmers
     assert_same_as_oracle(kc, ref)
