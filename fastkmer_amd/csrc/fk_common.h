@@ -97,7 +97,9 @@ FK_HD uint32_t bin_of_signature(uint32_t sig, const FastMod &f) { return fastmod
 // LDS hash count splits a bin's records into groups by it, and every
 // occurrence of a canonical k-mer has the same signature (the norm is
 // strand-symmetric), so a k-mer's occurrences all land in one group.
-FK_HD uint32_t fine_of_signature(uint32_t sig) { return (sig * 0x9E3779B1u) >> 26; }
+// The top six bits of the 31-bit bin hash: no second multiply per record (the bin takes hash32's
+// low bits for a power-of-two B, its residue otherwise).
+FK_HD uint32_t fine_of_signature(uint32_t sig) { return hash32(sig) >> 25; }
 
 // ---- canonical k-mers (getOrientation + readFromKmer, package.scala:721-728,
 // 174-295): canonical = min(forward, reverse complement) as 2k-bit integers,
