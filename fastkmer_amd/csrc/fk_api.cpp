@@ -382,7 +382,7 @@ struct fk_ctx {
     // piece is partitioned and expanded into its own key array while later pieces land; the job's
     // buckets are counted once over every piece's keys (no per-piece count, no merge)
     int piece_mode = 1;                          // FASTKMER_PIECE_MODE: 1 staged, 0 count + merge per piece
-    std::vector<double> st_cuts{0.45, 0.7, 0.85};  // piece ends of a staged job (FASTKMER_PIECE_CUTS)
+    std::vector<double> st_cuts{0.4, 0.7, 0.9};  // piece ends of a staged job (FASTKMER_PIECE_CUTS; 45 / 70 / 85 % measured 22.84 vs 22.77 ms)
     bool st_cuts_set = false;
     double st_one_level = 0.0;                   // FASTKMER_STAGED_ONE_LEVEL: one-pass expansion below this job fraction
     uint32_t st_np = 0;                          // pieces expanded in the current job
