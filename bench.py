@@ -374,7 +374,10 @@ def main() -> None:
                                "traffic": load_traffic(kname) if r0.fasta_bytes == 999_999_906 else None,
                                "bytes_alg_per_launch": r0.fasta_bytes, "ms_per_launch": t_k * 1e3,
                                "measured": "HIP events around each launch on the context's map stream "
-                                           "(HBM-resident leg)"}
+                                           "(HBM-resident leg)",
+                               "note": "priced against HBM for the contract; the measured limiter is VALU "
+                                       "issue (about 6.5e8 wave64 VALU instructions per GB at about 3.7 "
+                                       "cycles each per SIMD, profiles/r04b_pmc_split_map.txt)"}
         if n_ranks == 1 and not args.no_cpu_baseline and wl == "c2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_bytes, k, m, B, read_len, genome)
         print(json.dumps(out), flush=True)
