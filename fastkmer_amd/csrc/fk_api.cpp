@@ -309,8 +309,10 @@ struct fk_ctx {
     DevBuf map_vslots;            // split map: the parse kernel's valid streams for the passes (MAP_VSLOT_TILES tiles)
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
+    DevBuf lh_parents, lh_suboff, lh_part;  // spill rounds: parents partitioned by sub-item (k_ht_subpart)
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
     int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
+    int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
     int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
@@ -340,6 +342,7 @@ struct fk_ctx {
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
     PinBuf pin_up, pin_down, pin_merge;  // staging: chunk tables up, per-bin counts down, merge tables up
     PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
+    PinBuf pin_ht;                        // hash count: spilled parents down, spill-round items up
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
     bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
@@ -348,6 +351,10 @@ struct fk_ctx {
     // bin-ordered result, bin_off / h_bin_off per bin.  Readers gather a bin's buckets (fk_get_bin) or
     // the whole result (fk_write_bins); the pieces merged by count_piece need dense arrays (want_dense).
     bool gapped = false, dense_ready = false, want_dense = false;
+    // The LDS hash count's result stays in the bins' regions: local bin lb's distinct entries at
+    // h_ht_kbase[lb] of lh_okeys / lh_ocnt (no packing pass; fk_write_bins packs it once).
+    bool ht_regions = false;
+    std::vector<uint64_t> h_ht_kbase;
     const uint64_t *res_keys = nullptr;   // okb of the last sorted count (out_keys, or mid)
     const uint64_t *res_fs = nullptr;     // flag_scan of its bucket cut
     uint64_t res_nbuckets = 0;
@@ -585,6 +592,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 #endif
     const char *lh = getenv("FASTKMER_LDS_HT");
     if (lh && lh[0]) c->lh_mode = atoi(lh);
+    if (const char *sp = getenv("FASTKMER_HT_SUBPART"); sp && sp[0]) c->lh_subpart = atoi(sp);
     if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
         c->piece_bytes_set = true;
@@ -683,7 +691,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat, &c->map_vslots,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
-                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt,
+                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt, &c->lh_parents, &c->lh_suboff, &c->lh_part,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
@@ -702,6 +710,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->pin_down.release();
     c->pin_merge.release();
     c->pin_tier.release();
+    c->pin_ht.release();
     c->file_pin[0].release();
     c->file_pin[1].release();
     if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
@@ -762,7 +771,7 @@ FK_EXPORT int32_t fk_num_bins(const fk_ctx *c) { return c ? c->Bc : 0; }
 static void reset_results(fk_ctx *c) {
     c->mapped = false;
     c->have_result = false;
-    c->gapped = c->dense_ready = false;
+    c->gapped = c->dense_ready = c->ht_regions = false;
     c->distinct = 0;
     c->h_bin_off.clear();
 }
@@ -1906,69 +1915,94 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
                                   nlb, d_flog, d_rec_base, d_km_base, d_gbase, Hr, Hk, c->lh_off.as<uint64_t>(),
                                   groups, c->lh_recs.as<uint64_t>(), s));
     unsigned long long *bin_cnt = c->table_off.as<unsigned long long>();
-    unsigned long long *sp_total = c->misc.as<unsigned long long>();
+    unsigned long long *sp_total = c->misc.as<unsigned long long>();  // [0] keys spilled, [1] spilled groups
     HIP_TRY(hipMemsetAsync(bin_cnt, 0, ((uint64_t)nlb + 1) * 8, s));
-    HIP_TRY(hipMemsetAsync(sp_total, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
     FK_TRY(ensure(c->lh_sp[0], (uint64_t)ngroups * 4 + 64));
     HIP_TRY(launch_ht_combine(c->W, c->lh_recs.as<uint64_t>(), groups, nullptr, ngroups, c->cfg.k, 0,
                               c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
                               c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe));
-    uint64_t spilled = 0;
-    HIP_TRY(hipMemcpyAsync(&spilled, sp_total, 8, hipMemcpyDeviceToHost, s));
+    // the groups that spilled, listed on the device (a parent each: its spill range and count)
+    FK_TRY(ensure(c->lh_parents, (uint64_t)ngroups * sizeof(LhItem) + 64));
+    HIP_TRY(launch_ht_spill_list(groups, c->lh_sp[0].as<uint32_t>(), ngroups, c->lh_parents.as<LhItem>(),
+                                 sp_total + 1, s));
+    if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    HIP_TRY(hipMemcpyAsync(c->pin_ht.p, sp_total, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    uint64_t spilled = c->pin_ht.as<uint64_t>()[0];
+    const uint64_t nspill_groups = c->pin_ht.as<uint64_t>()[1];
     c->stats.ht_spilled = spilled;
     // spill rounds: each spilled range (a parent) is split by a salted key hash into sub-items of
     // about per_group keys, so one heavy signature (a group far beyond a table) takes one more
     // round instead of one per table's worth of keys.  The sub-items of a parent partition its
     // keys, so they share one spill range of the parent's size (a cursor per parent): a round's
-    // spill space is at most the previous round's spilled keys.
+    // spill space is at most the previous round's spilled keys.  Parents of 2..2^LH_SUB_MAXLOG
+    // sub-items are first partitioned by sub-item (k_ht_subpart), so a sub-item reads its keys only.
     std::vector<LhItem> prev, items;
-    {
-        std::vector<uint32_t> cnt(ngroups);
-        if (spilled) HIP_TRY(hipMemcpy(cnt.data(), c->lh_sp[0].p, (uint64_t)ngroups * 4, hipMemcpyDeviceToHost));
-        std::vector<LhGroup> hg;
-        if (spilled) {
-            hg.resize(ngroups);
-            HIP_TRY(hipMemcpy(hg.data(), groups, (uint64_t)ngroups * sizeof(LhGroup), hipMemcpyDeviceToHost));
-        }
-        for (uint32_t g = 0; spilled && g < ngroups; ++g)
-            if (cnt[g]) prev.push_back(LhItem{hg[g].km_begin, 0, cnt[g], hg[g].lbin, 0, 0, 0, 0});
+    if (spilled) {
+        if (c->pin_ht.ensure(nspill_groups * sizeof(LhItem))) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+        HIP_TRY(hipMemcpyAsync(c->pin_ht.p, c->lh_parents.p, nspill_groups * sizeof(LhItem), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        prev.assign(c->pin_ht.as<LhItem>(), c->pin_ht.as<LhItem>() + nspill_groups);
     }
     int cur = 0, rounds = 1;
     while (spilled) {
         if (++rounds > 16) return set_err(FK_E_DEVICE, "hash count: spill rounds do not converge");
         const int nxt = cur ^ 1;
         items.clear();
-        uint64_t out = 0;
+        uint64_t out = 0, src_end = 0;
+        uint32_t nsub_off = 0;
         std::vector<uint64_t> region(prev.size());
+        std::vector<LhItem> parts;  // parents split into sub-items: pre-partitioned by k_ht_subpart
         for (uint32_t pi = 0; pi < (uint32_t)prev.size(); ++pi) {
             const LhItem &p = prev[pi];
             int sl = 0;
             while (sl < 16 && (double)(1u << sl) * per_group < (double)p.in_cnt) ++sl;
+            uint32_t pad = LH_NOPART;
+            if (sl >= 1 && sl <= LH_SUB_MAXLOG && c->lh_subpart) {
+                pad = nsub_off;
+                nsub_off += (1u << sl) + 1u;
+                parts.push_back(LhItem{p.in_base, 0, p.in_cnt, p.lbin, 0, (uint32_t)sl, pi, pad});
+                src_end = std::max(src_end, p.in_base + p.in_cnt);
+            }
             for (uint32_t sub = 0; sub < (1u << sl); ++sub)
-                items.push_back(LhItem{p.in_base, out, p.in_cnt, p.lbin, sub, (uint32_t)sl, pi, 0});
+                items.push_back(LhItem{p.in_base, out, p.in_cnt, p.lbin, sub, (uint32_t)sl, pi, pad});
             region[pi] = out;
             out += p.in_cnt;  // the parent's sub-items spill at most its keys, together
         }
         const uint32_t ni = (uint32_t)items.size(), np = (uint32_t)prev.size();
-        FK_TRY(ensure(c->lh_spill[nxt], out * 8 * KW + 64));
-        FK_TRY(ensure(c->lh_items, (uint64_t)ni * sizeof(LhItem) + 64));
+        // one pinned upload: the items, then the partitioned parents
+        const size_t up_bytes = ((size_t)ni + parts.size()) * sizeof(LhItem);
+        if (c->pin_ht.ensure(up_bytes)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+        std::memcpy(c->pin_ht.p, items.data(), (size_t)ni * sizeof(LhItem));
+        std::memcpy(c->pin_ht.as<LhItem>() + ni, parts.data(), parts.size() * sizeof(LhItem));
+        FK_TRY(ensure(c->lh_items, up_bytes + 64));
         LhItem *d_items = c->lh_items.as<LhItem>();
+        HIP_TRY(hipMemcpyAsync(d_items, c->pin_ht.p, up_bytes, hipMemcpyHostToDevice, s));
+        if (!parts.empty()) {
+            FK_TRY(ensure(c->lh_suboff, (uint64_t)nsub_off * 4 + 64));
+            FK_TRY(ensure(c->lh_part, src_end * 8 * KW + 64));
+            HIP_TRY(launch_ht_subpart((int)KW, c->lh_spill[cur].as<uint64_t>(), d_items + ni, (uint32_t)parts.size(),
+                                      (uint32_t)rounds, c->lh_part.as<uint64_t>(), c->lh_suboff.as<uint32_t>(), s));
+        }
+        FK_TRY(ensure(c->lh_spill[nxt], out * 8 * KW + 64));
         FK_TRY(ensure(c->lh_sp[nxt], (uint64_t)np * 4 + 64));
-        HIP_TRY(hipMemcpyAsync(d_items, items.data(), (uint64_t)ni * sizeof(LhItem), hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemsetAsync(c->lh_sp[nxt].p, 0, (uint64_t)np * 4, s));
         HIP_TRY(hipMemsetAsync(sp_total, 0, 8, s));
         HIP_TRY(launch_ht_combine(c->W, c->lh_spill[cur].as<uint64_t>(), groups, d_items, ni, c->cfg.k,
                                   (uint32_t)rounds, c->lh_spill[nxt].as<uint64_t>(), c->lh_sp[nxt].as<uint32_t>(),
                                   sp_total, d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(),
-                                  c->lh_ocnt.as<uint32_t>(), s));
-        HIP_TRY(hipMemcpyAsync(&spilled, sp_total, 8, hipMemcpyDeviceToHost, s));
+                                  c->lh_ocnt.as<uint32_t>(), s, 0, c->lh_part.as<uint64_t>(),
+                                  c->lh_suboff.as<uint32_t>()));
+        if (c->pin_ht.ensure(8 + (size_t)np * 4)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+        HIP_TRY(hipMemcpyAsync(c->pin_ht.p, sp_total, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->pin_ht.as<uint8_t>() + 8, c->lh_sp[nxt].p, (uint64_t)np * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        spilled = c->pin_ht.as<uint64_t>()[0];
         c->stats.ht_spilled += spilled;
         std::vector<LhItem> next;
         if (spilled) {
-            std::vector<uint32_t> cnt(np);
-            HIP_TRY(hipMemcpy(cnt.data(), c->lh_sp[nxt].p, (uint64_t)np * 4, hipMemcpyDeviceToHost));
+            const uint32_t *cnt = reinterpret_cast<const uint32_t *>(c->pin_ht.as<uint8_t>() + 8);
             for (uint32_t pi = 0; pi < np; ++pi)
                 if (cnt[pi]) next.push_back(LhItem{region[pi], 0, cnt[pi], prev[pi].lbin, 0, 0, 0, 0});
         }
@@ -1982,11 +2016,11 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     uint64_t distinct = 0;
     HIP_TRY(hipMemcpyAsync(&distinct, c->bin_off.as<uint64_t>() + nlb, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    FK_TRY(ensure(c->dense_keys, distinct * 8 * KW + 64));
-    FK_TRY(ensure(c->dense_counts, distinct * 4 + 64));
-    HIP_TRY(launch_ht_gather((int)KW, d_km_base, c->bin_off.as<uint64_t>(), nlb, c->lh_okeys.as<uint64_t>(),
-                             c->lh_ocnt.as<uint32_t>(), c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(),
-                             s));
+    // the result stays in the bins' regions (measured: packing it densely cost 17.9 ms of a 67 ms
+    // count at the configs[3] shape); materialize_dense packs it for fk_write_bins
+    c->ht_regions = true;
+    c->dense_ready = false;
+    c->h_ht_kbase = km_base;
     c->distinct = distinct;
     if (nkm) c->lh_ratio = std::min(1.0, std::max(0.02, (double)distinct / (double)nkm));
     return FK_OK;
@@ -3291,8 +3325,19 @@ FK_EXPORT int fk_bin_sizes(fk_ctx *c, uint64_t *out) {
 
 // A bucket-major result made dense (fk_write_bins): the buckets' outputs compacted in bin order.
 static int materialize_dense(fk_ctx *c) {
-    if (!c->gapped || c->dense_ready) return FK_OK;
+    if (!(c->gapped || c->ht_regions) || c->dense_ready) return FK_OK;
     hipStream_t s = c->stream;
+    if (c->ht_regions) {  // the hash count's bin regions packed in bin order
+        FK_TRY(ensure(c->dense_keys, c->distinct * 8 * c->KW + 64));
+        FK_TRY(ensure(c->dense_counts, c->distinct * 4 + 64));
+        const uint64_t *d_km_base = c->lh_meta.as<uint64_t>() + (c->nlb + 1);
+        HIP_TRY(launch_ht_gather(c->KW, d_km_base, c->bin_off.as<uint64_t>(), c->nlb, c->lh_okeys.as<uint64_t>(),
+                                 c->lh_ocnt.as<uint32_t>(), c->dense_keys.as<uint64_t>(),
+                                 c->dense_counts.as<uint32_t>(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->dense_ready = true;
+        return FK_OK;
+    }
     FK_TRY(ensure(c->dense_keys, c->distinct * 8 * c->KW));
     FK_TRY(ensure(c->dense_counts, c->distinct * 4));
     HIP_TRY(launch_bucket_compact(c->KW, c->res_keys, c->out_counts.as<uint32_t>(), c->buckets.as<Bucket>(),
@@ -3333,6 +3378,13 @@ FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *count
     *n = (size_t)cnt;
     if (cnt == 0) return FK_OK;
     if (cap < cnt) return set_err(FK_E_RANGE, "bin %d has %llu k-mers, buffer holds %zu", bin, (unsigned long long)cnt, cap);
+    if (c->ht_regions && !c->dense_ready) {  // the bin's region of the hash count's output
+        const uint64_t r0 = c->h_ht_kbase[lb];
+        if (keys)
+            HIP_TRY(hipMemcpy(keys, c->lh_okeys.as<uint64_t>() + r0 * c->KW, cnt * 8 * c->KW, hipMemcpyDeviceToHost));
+        if (counts) HIP_TRY(hipMemcpy(counts, c->lh_ocnt.as<uint32_t>() + r0, cnt * 4, hipMemcpyDeviceToHost));
+        return FK_OK;
+    }
     if (c->gapped && !c->dense_ready) {
         FK_TRY(ensure(c->gather_keys, cnt * 8 * c->KW));
         FK_TRY(ensure(c->gather_counts, cnt * 4));

@@ -280,14 +280,28 @@ struct LhItem {            // one work item of a spill round: the keys of a pare
     uint64_t in_base;     // group, or of a parent of the previous round) whose salted key hash selects `sub`
     uint64_t out_base;    // the parent's spill range (in_cnt slots, shared by its 2^slog sub-items)
     uint32_t in_cnt, lbin, sub, slog;
-    uint32_t parent, pad; // spill cursor of the parent (sp_cnt[parent])
+    uint32_t parent;      // spill cursor of the parent (sp_cnt[parent])
+    uint32_t pad;         // sub_off index of the parent's partitioned sub-ranges (k_ht_subpart), or
+                          // LH_NOPART: the item reads the whole parent range and filters by hash
 };
+constexpr uint32_t LH_NOPART = ~0u;
+constexpr int LH_SUB_MAXLOG = 12;  // parents split into at most 2^12 sub-items are pre-partitioned
+// spill-round pre-partition: parents[0..np) (slog >= 1, pad = sub_off base) -> each parent's keys
+// copied to dst at the same offsets, grouped by the round's salted key hash & (2^slog - 1);
+// sub_off[pad + s] = the first key of sub-range s relative to in_base (2^slog + 1 entries)
+// the groups of round 1 that spilled (sp_cnt[g] > 0) as parents of the next round, in any order:
+// out[i] = {km_begin, 0, sp_cnt[g], lbin, 0, 0, 0, 0}; *n_out += their number
+hipError_t launch_ht_spill_list(const LhGroup *groups, const uint32_t *sp_cnt, uint32_t ngroups, LhItem *out,
+                                unsigned long long *n_out, hipStream_t s);
+hipError_t launch_ht_subpart(int KW, const uint64_t *src, const LhItem *parents, uint32_t np, uint32_t salt,
+                             uint64_t *dst, uint32_t *sub_off, hipStream_t s);
 // items == null: round 1 over groups[0..n), sp_cnt[g] = keys group g spilled; else a spill round
 // over items[0..n), sp_cnt[parent] = the spill cursor of each parent (zeroed by the caller)
 hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, const LhItem *items, uint32_t n,
                              int k, uint32_t salt, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
                              const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys, uint32_t *ocnt,
-                             hipStream_t s, int probe = 0);
+                             hipStream_t s, int probe = 0, const uint64_t *psrc = nullptr,
+                             const uint32_t *sub_off = nullptr);
 hipError_t launch_ht_gather(int KW, const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb,
                             const uint64_t *okeys, const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt,
                             hipStream_t s);

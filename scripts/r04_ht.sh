@@ -4,12 +4,14 @@
 # (lib_htold, -DFK_HT_PERKMER=0), and rocprofv3 kernel stats of the product run.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd $R; O=$R/gpurun_out/ht; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_hash.py > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_hash.py tests/test_gpu_write.py tests/test_gpu_parity.py > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -3 $O/tests.txt
 timeout -k 10 300 python -u scripts/ht_probe.py > $O/probe.txt 2>&1 || { tail -20 $O/probe.txt; exit 1; }
 cat $O/probe.txt
 FASTKMER_LIB=$R/fastkmer_amd/lib_htold/libfastkmer.so timeout -k 10 300 python -u scripts/ht_probe.py > $O/probe_old.txt 2>&1 || { tail -20 $O/probe_old.txt; exit 1; }
 cat $O/probe_old.txt
+FASTKMER_HT_SUBPART=0 timeout -k 10 300 python -u scripts/ht_probe.py > $O/probe_nosub.txt 2>&1 || { tail -20 $O/probe_nosub.txt; exit 1; }
+cat $O/probe_nosub.txt
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 $R/scripts/ht_probe.py > $O/p.log 2>&1 || { tail -20 $O/p.log; exit 1; }
 python3 $R/scripts/kstats.py $O/p/run_kernel_stats.csv 16
