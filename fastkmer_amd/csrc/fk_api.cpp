@@ -309,7 +309,7 @@ struct fk_ctx {
     DevBuf map_vslots;            // split map: the parse kernel's valid streams for the passes (MAP_VSLOT_TILES tiles)
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
-    DevBuf lh_parents, lh_suboff, lh_part;  // spill rounds: parents partitioned by sub-item (k_ht_subpart)
+    DevBuf lh_parents, lh_parents2, lh_plan, lh_suboff, lh_part;  // spill rounds: parents, their plan, sub-ranges
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
     int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
     int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
@@ -691,7 +691,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat, &c->map_vslots,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
-                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt, &c->lh_parents, &c->lh_suboff, &c->lh_part,
+                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt, &c->lh_parents, &c->lh_parents2, &c->lh_plan, &c->lh_suboff, &c->lh_part,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
@@ -1927,86 +1927,62 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     HIP_TRY(launch_ht_spill_list(groups, c->lh_sp[0].as<uint32_t>(), ngroups, c->lh_parents.as<LhItem>(),
                                  sp_total + 1, s));
     if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-    HIP_TRY(hipMemcpyAsync(c->pin_ht.p, sp_total, 16, hipMemcpyDeviceToHost, s));
+    uint64_t *const pin = c->pin_ht.as<uint64_t>();
+    HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    uint64_t spilled = c->pin_ht.as<uint64_t>()[0];
-    const uint64_t nspill_groups = c->pin_ht.as<uint64_t>()[1];
+    uint64_t spilled = pin[0], np = pin[1];
     c->stats.ht_spilled = spilled;
-    // spill rounds: each spilled range (a parent) is split by a salted key hash into sub-items of
-    // about per_group keys, so one heavy signature (a group far beyond a table) takes one more
-    // round instead of one per table's worth of keys.  The sub-items of a parent partition its
-    // keys, so they share one spill range of the parent's size (a cursor per parent): a round's
-    // spill space is at most the previous round's spilled keys.  Parents of 2..2^LH_SUB_MAXLOG
-    // sub-items are first partitioned by sub-item (k_ht_subpart), so a sub-item reads its keys only.
-    std::vector<LhItem> prev, items;
-    if (spilled) {
-        if (c->pin_ht.ensure(nspill_groups * sizeof(LhItem))) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-        HIP_TRY(hipMemcpyAsync(c->pin_ht.p, c->lh_parents.p, nspill_groups * sizeof(LhItem), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        prev.assign(c->pin_ht.as<LhItem>(), c->pin_ht.as<LhItem>() + nspill_groups);
-    }
+    // spill rounds, planned on the device (the host reads three totals per round): each spilled
+    // range (a parent) is split by a salted key hash into 2^slog sub-items of about per_group keys,
+    // so one heavy signature (a group far beyond a table) takes one more round instead of one per
+    // table's worth of keys.  The sub-items of a parent partition its keys, so they share one
+    // spill range of the parent's size (a cursor per parent): a round's spill space is at most the
+    // previous round's spilled keys.  Parents of 2..2^LH_SUB_MAXLOG sub-items are first
+    // partitioned by sub-item (k_ht_subpart), so a sub-item reads its own keys only.  A round's
+    // parents are at most the previous round's (one spill range each).
+    if (spilled) FK_TRY(ensure(c->lh_parents2, np * sizeof(LhItem) + 64));
+    LhItem *par = c->lh_parents.as<LhItem>(), *par_next = c->lh_parents2.as<LhItem>();
     int cur = 0, rounds = 1;
     while (spilled) {
         if (++rounds > 16) return set_err(FK_E_DEVICE, "hash count: spill rounds do not converge");
         const int nxt = cur ^ 1;
-        items.clear();
-        uint64_t out = 0, src_end = 0;
-        uint32_t nsub_off = 0;
-        std::vector<uint64_t> region(prev.size());
-        std::vector<LhItem> parts;  // parents split into sub-items: pre-partitioned by k_ht_subpart
-        for (uint32_t pi = 0; pi < (uint32_t)prev.size(); ++pi) {
-            const LhItem &p = prev[pi];
-            int sl = 0;
-            while (sl < 16 && (double)(1u << sl) * per_group < (double)p.in_cnt) ++sl;
-            uint32_t pad = LH_NOPART;
-            if (sl >= 1 && sl <= LH_SUB_MAXLOG && c->lh_subpart) {
-                pad = nsub_off;
-                nsub_off += (1u << sl) + 1u;
-                parts.push_back(LhItem{p.in_base, 0, p.in_cnt, p.lbin, 0, (uint32_t)sl, pi, pad});
-                src_end = std::max(src_end, p.in_base + p.in_cnt);
-            }
-            for (uint32_t sub = 0; sub < (1u << sl); ++sub)
-                items.push_back(LhItem{p.in_base, out, p.in_cnt, p.lbin, sub, (uint32_t)sl, pi, pad});
-            region[pi] = out;
-            out += p.in_cnt;  // the parent's sub-items spill at most its keys, together
-        }
-        const uint32_t ni = (uint32_t)items.size(), np = (uint32_t)prev.size();
-        // one pinned upload: the items, then the partitioned parents
-        const size_t up_bytes = ((size_t)ni + parts.size()) * sizeof(LhItem);
-        if (c->pin_ht.ensure(up_bytes)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-        std::memcpy(c->pin_ht.p, items.data(), (size_t)ni * sizeof(LhItem));
-        std::memcpy(c->pin_ht.as<LhItem>() + ni, parts.data(), parts.size() * sizeof(LhItem));
-        FK_TRY(ensure(c->lh_items, up_bytes + 64));
-        LhItem *d_items = c->lh_items.as<LhItem>();
-        HIP_TRY(hipMemcpyAsync(d_items, c->pin_ht.p, up_bytes, hipMemcpyHostToDevice, s));
-        if (!parts.empty()) {
-            FK_TRY(ensure(c->lh_suboff, (uint64_t)nsub_off * 4 + 64));
-            FK_TRY(ensure(c->lh_part, src_end * 8 * KW + 64));
-            HIP_TRY(launch_ht_subpart((int)KW, c->lh_spill[cur].as<uint64_t>(), d_items + ni, (uint32_t)parts.size(),
-                                      (uint32_t)rounds, c->lh_part.as<uint64_t>(), c->lh_suboff.as<uint32_t>(), s));
-        }
+        FK_TRY(ensure(c->lh_plan, (6 * np + 4) * 8));
+        uint64_t *const pl = c->lh_plan.as<uint64_t>();
+        uint64_t *const cnt = pl, *const nsub = pl + np, *const npad = pl + 2 * np, *const region = pl + 3 * np,
+                       *const item_off = pl + 4 * np, *const pad_off = pl + 5 * np, *const tot = pl + 6 * np;
+        HIP_TRY(launch_ht_plan(par, (uint32_t)np, per_group, c->lh_subpart, cnt, nsub, npad, s));
+        HIP_TRY(scan_excl_sum_u64(cnt, region, np, tot, c->ws, s));
+        HIP_TRY(scan_excl_sum_u64(nsub, item_off, np, tot + 1, c->ws, s));
+        HIP_TRY(scan_excl_sum_u64(npad, pad_off, np, tot + 2, c->ws, s));
+        HIP_TRY(hipMemcpyAsync(pin, tot, 24, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint64_t out = pin[0], ni = pin[1], nsub_off = pin[2];
+        if (ni > 0xffffffffull) return set_err(FK_E_DEVICE, "hash count: %llu spill items", (unsigned long long)ni);
+        FK_TRY(ensure(c->lh_items, ni * sizeof(LhItem) + 64));
+        FK_TRY(ensure(c->lh_suboff, nsub_off * 4 + 64));
+        if (nsub_off) FK_TRY(ensure(c->lh_part, c->lh_spill[cur].bytes));
         FK_TRY(ensure(c->lh_spill[nxt], out * 8 * KW + 64));
-        FK_TRY(ensure(c->lh_sp[nxt], (uint64_t)np * 4 + 64));
-        HIP_TRY(hipMemsetAsync(c->lh_sp[nxt].p, 0, (uint64_t)np * 4, s));
-        HIP_TRY(hipMemsetAsync(sp_total, 0, 8, s));
-        HIP_TRY(launch_ht_combine(c->W, c->lh_spill[cur].as<uint64_t>(), groups, d_items, ni, c->cfg.k,
+        FK_TRY(ensure(c->lh_sp[nxt], np * 4 + 64));
+        LhItem *d_items = c->lh_items.as<LhItem>();
+        HIP_TRY(launch_ht_items(par, (uint32_t)np, region, item_off, pad_off, npad, d_items, s));
+        if (nsub_off)
+            HIP_TRY(launch_ht_subpart((int)KW, c->lh_spill[cur].as<uint64_t>(), par, (uint32_t)np, (uint32_t)rounds,
+                                      c->lh_part.as<uint64_t>(), c->lh_suboff.as<uint32_t>(), s));
+        HIP_TRY(hipMemsetAsync(c->lh_sp[nxt].p, 0, np * 4, s));
+        HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
+        HIP_TRY(launch_ht_combine(c->W, c->lh_spill[cur].as<uint64_t>(), groups, d_items, (uint32_t)ni, c->cfg.k,
                                   (uint32_t)rounds, c->lh_spill[nxt].as<uint64_t>(), c->lh_sp[nxt].as<uint32_t>(),
                                   sp_total, d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(),
                                   c->lh_ocnt.as<uint32_t>(), s, 0, c->lh_part.as<uint64_t>(),
                                   c->lh_suboff.as<uint32_t>()));
-        if (c->pin_ht.ensure(8 + (size_t)np * 4)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-        HIP_TRY(hipMemcpyAsync(c->pin_ht.p, sp_total, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(c->pin_ht.as<uint8_t>() + 8, c->lh_sp[nxt].p, (uint64_t)np * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(launch_ht_next_parents(par, (uint32_t)np, region, c->lh_sp[nxt].as<uint32_t>(), par_next, sp_total + 1,
+                                       s));
+        HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        spilled = c->pin_ht.as<uint64_t>()[0];
+        spilled = pin[0];
+        np = pin[1];
         c->stats.ht_spilled += spilled;
-        std::vector<LhItem> next;
-        if (spilled) {
-            const uint32_t *cnt = reinterpret_cast<const uint32_t *>(c->pin_ht.as<uint8_t>() + 8);
-            for (uint32_t pi = 0; pi < np; ++pi)
-                if (cnt[pi]) next.push_back(LhItem{region[pi], 0, cnt[pi], prev[pi].lbin, 0, 0, 0, 0});
-        }
-        prev.swap(next);
+        std::swap(par, par_next);
         cur = nxt;
     }
     c->stats.ht_rounds = (uint64_t)rounds;

@@ -286,13 +286,25 @@ struct LhItem {            // one work item of a spill round: the keys of a pare
 };
 constexpr uint32_t LH_NOPART = ~0u;
 constexpr int LH_SUB_MAXLOG = 12;  // parents split into at most 2^12 sub-items are pre-partitioned
-// spill-round pre-partition: parents[0..np) (slog >= 1, pad = sub_off base) -> each parent's keys
+// spill-round pre-partition: parents[0..np) with pad != LH_NOPART (pad = sub_off base) -> their keys
 // copied to dst at the same offsets, grouped by the round's salted key hash & (2^slog - 1);
 // sub_off[pad + s] = the first key of sub-range s relative to in_base (2^slog + 1 entries)
 // the groups of round 1 that spilled (sp_cnt[g] > 0) as parents of the next round, in any order:
 // out[i] = {km_begin, 0, sp_cnt[g], lbin, 0, 0, 0, 0}; *n_out += their number
 hipError_t launch_ht_spill_list(const LhGroup *groups, const uint32_t *sp_cnt, uint32_t ngroups, LhItem *out,
                                 unsigned long long *n_out, hipStream_t s);
+// spill-round plan over np parents (one thread each): parents[p].slog = sub-item bits (2^slog
+// sub-items of about per_group keys); cnt = in_cnt, nsub = 2^slog, npad = 2^slog + 1 for a parent
+// pre-partitioned by k_ht_subpart (subpart != 0, 1 <= slog <= LH_SUB_MAXLOG), else 0
+hipError_t launch_ht_plan(LhItem *parents, uint32_t np, double per_group, int subpart, uint64_t *cnt, uint64_t *nsub,
+                          uint64_t *npad, hipStream_t s);
+// the round's items from the scanned plan (region = spill range, item_off, pad_off = sub_off base);
+// parents[p].pad = pad_off[p] or LH_NOPART
+hipError_t launch_ht_items(LhItem *parents, uint32_t np, const uint64_t *region, const uint64_t *item_off,
+                           const uint64_t *pad_off, const uint64_t *npad, LhItem *items, hipStream_t s);
+// the parents that spilled again (sp_cnt[p] > 0) as the next round's: {region[p], 0, sp_cnt[p], lbin}
+hipError_t launch_ht_next_parents(const LhItem *parents, uint32_t np, const uint64_t *region, const uint32_t *sp_cnt,
+                                  LhItem *out, unsigned long long *n_out, hipStream_t s);
 hipError_t launch_ht_subpart(int KW, const uint64_t *src, const LhItem *parents, uint32_t np, uint32_t salt,
                              uint64_t *dst, uint32_t *sub_off, hipStream_t s);
 // items == null: round 1 over groups[0..n), sp_cnt[g] = keys group g spilled; else a spill round
