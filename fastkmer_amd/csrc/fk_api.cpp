@@ -309,10 +309,11 @@ struct fk_ctx {
     DevBuf map_vslots;            // split map: the parse kernel's valid streams for the passes (MAP_VSLOT_TILES tiles)
     // hash count in LDS tables (fk_count_lds.inc)
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
-    DevBuf lh_parents, lh_parents2, lh_plan, lh_suboff, lh_part;  // spill rounds: parents, their plan, sub-ranges
+    DevBuf lh_parents, lh_parents2, lh_plan, lh_suboff, lh_part, lh_glist;  // spill rounds: parents, their plan, sub-ranges
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
     int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
     int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
+    uint32_t lh_big_thr = 0;      // FASTKMER_HT_BIG: k > 32, groups of more k-mers take 6144-slot tables (0: none)
     int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
@@ -593,6 +594,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     const char *lh = getenv("FASTKMER_LDS_HT");
     if (lh && lh[0]) c->lh_mode = atoi(lh);
     if (const char *sp = getenv("FASTKMER_HT_SUBPART"); sp && sp[0]) c->lh_subpart = atoi(sp);
+    if (const char *hb = getenv("FASTKMER_HT_BIG"); hb && hb[0]) c->lh_big_thr = (uint32_t)strtoul(hb, nullptr, 10);
     if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
         c->piece_bytes_set = true;
@@ -691,7 +693,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat, &c->map_vslots,
                       &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
-                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt, &c->lh_parents, &c->lh_parents2, &c->lh_plan, &c->lh_suboff, &c->lh_part,
+                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt, &c->lh_parents, &c->lh_parents2, &c->lh_plan, &c->lh_suboff, &c->lh_part, &c->lh_glist,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
@@ -1919,15 +1921,33 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     HIP_TRY(hipMemsetAsync(bin_cnt, 0, ((uint64_t)nlb + 1) * 8, s));
     HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
     FK_TRY(ensure(c->lh_sp[0], (uint64_t)ngroups * 4 + 64));
+    if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+    uint64_t *const pin = c->pin_ht.as<uint64_t>();
+    // 128-bit keys: the groups of more than lh_big_thr k-mers take 6144-slot tables (one workgroup
+    // per CU) instead of spilling most of their keys from the 2048-slot ones
+    uint64_t nbig = 0;
+    const uint32_t big_thr = KW == 2 ? c->lh_big_thr : 0u;
+    if (big_thr) {
+        FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 4 + 64));
+        HIP_TRY(launch_ht_big_list(groups, ngroups, big_thr, c->lh_glist.as<uint32_t>(), sp_total + 1, s));
+        HIP_TRY(hipMemcpyAsync(pin, sp_total + 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemsetAsync(sp_total + 1, 0, 8, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        nbig = pin[0];
+    }
+    c->stats.ht_big_groups = nbig;
     HIP_TRY(launch_ht_combine(c->W, c->lh_recs.as<uint64_t>(), groups, nullptr, ngroups, c->cfg.k, 0,
                               c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
-                              c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe));
+                              c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe, nullptr, nullptr,
+                              nbig ? big_thr : 0u));
+    if (nbig)
+        HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
+                                         c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
+                                         d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
     // the groups that spilled, listed on the device (a parent each: its spill range and count)
     FK_TRY(ensure(c->lh_parents, (uint64_t)ngroups * sizeof(LhItem) + 64));
     HIP_TRY(launch_ht_spill_list(groups, c->lh_sp[0].as<uint32_t>(), ngroups, c->lh_parents.as<LhItem>(),
                                  sp_total + 1, s));
-    if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-    uint64_t *const pin = c->pin_ht.as<uint64_t>();
     HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     uint64_t spilled = pin[0], np = pin[1];

@@ -89,6 +89,7 @@ typedef struct fk_stats {
                                   count merged them with the later pieces' k-mers */
     uint64_t block_buckets;    /* buckets above the wave tier of at most 2048 keys (mid wave tier, block kernel) */
     uint64_t big_buckets;      /* buckets above 2048 keys (the big-table kernel, then the large path) */
+    uint64_t ht_big_groups;    /* useHT, k > 32: groups counted in the 6144-slot tables (FASTKMER_HT_BIG) */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

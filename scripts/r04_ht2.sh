@@ -12,6 +12,10 @@ for v in base htn512 htp1 htp2; do
   echo "== $v"; cat $O/probe_$v.txt | grep LDS
 done
 unset FASTKMER_LIB
+for t in 1800 2600; do
+  FASTKMER_HT_BIG=$t timeout -k 10 300 python -u scripts/ht_probe.py > $O/probe_big$t.txt 2>&1 || { tail -20 $O/probe_big$t.txt; exit 1; }
+  echo "== big $t"; grep LDS $O/probe_big$t.txt
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 $R/scripts/ht_probe.py > $O/p.log 2>&1 || { tail -20 $O/p.log; exit 1; }
 python3 $R/scripts/kstats.py $O/p/run_kernel_stats.csv 20

@@ -40,3 +40,20 @@ def test_ht_two_word_lds_tables_vs_oracle(k, m, B):
         assert_same_as_oracle(kc, ref, ordered=False)
         if B == 1:
             assert st["ht_rounds"] > 1
+
+
+@pytest.mark.parametrize("k,m,B,thr", [(55, 12, 64, 600), (63, 15, 64, 1500), (55, 12, 1, 2000)])
+def test_ht_heavy_group_tables_vs_oracle(monkeypatch, k, m, B, thr):
+    # k > 32 with FASTKMER_HT_BIG: groups of more than thr k-mers take the 6144-slot tables
+    # (k_ht_combine128<false, 1024, 6144> over the device-listed heavy groups), the rest the
+    # 2048-slot ones; B = 1 still spills past the big tables
+    monkeypatch.setenv("FASTKMER_HT_BIG", str(thr))
+    fasta = fk.synth_fasta(40_000, 150, 20_000_000, seed=0xB3 + k + B)
+    with fk.KmerCounter(k, m, 3, B, use_ht=True) as kc:
+        kc.ingest(fasta)
+        kc.finish()
+        st = kc.stats()
+        ref = oracle.OracleResult(fasta, k, m, B)
+        assert st["kmers"] == ref.total_kmers and st["distinct"] == ref.distinct
+        assert_same_as_oracle(kc, ref, ordered=False)
+        assert st["ht_big_groups"] > 0, st
