@@ -313,7 +313,7 @@ struct fk_ctx {
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
     int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
     int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
-    uint32_t lh_big_thr = 0;      // FASTKMER_HT_BIG: k > 32, groups of more k-mers take 6144-slot tables (0: none)
+    uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG: k > 32, groups of more k-mers take 6144-slot tables (0: none)
     int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
