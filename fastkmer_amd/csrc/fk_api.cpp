@@ -313,7 +313,8 @@ struct fk_ctx {
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
     int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
     int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
-    uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG: k > 32, groups of more k-mers take 6144-slot tables (0: none)
+    uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG: k > 32, groups of more k-mers take larger tables (0: none)
+    uint32_t lh_huge_thr = 0;     // FASTKMER_HT_HUGE: groups up to this many k-mers take 3072 slots, above 6144 (0: all 6144)
     int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
@@ -392,6 +393,7 @@ struct fk_ctx {
     int piece_mode = 1;                          // FASTKMER_PIECE_MODE: 1 staged, 0 count + merge per piece
     std::vector<double> st_cuts{0.4, 0.7, 0.9};  // piece ends of a staged job (FASTKMER_PIECE_CUTS; 45 / 70 / 85 % measured 22.84 vs 22.77 ms)
     bool st_cuts_set = false;
+    int xch_cuts = 1;  // FASTKMER_XCH_CUTS=0: the exchange path stages every quarter of the job (round 3)
     double st_one_level = 0.0;                   // FASTKMER_STAGED_ONE_LEVEL: one-pass expansion below this job fraction
     uint32_t st_np = 0;                          // pieces expanded in the current job
     SortedPlan st_plan;                          // the job's cells (fixed by its first piece)
@@ -595,6 +597,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (lh && lh[0]) c->lh_mode = atoi(lh);
     if (const char *sp = getenv("FASTKMER_HT_SUBPART"); sp && sp[0]) c->lh_subpart = atoi(sp);
     if (const char *hb = getenv("FASTKMER_HT_BIG"); hb && hb[0]) c->lh_big_thr = (uint32_t)strtoul(hb, nullptr, 10);
+    if (const char *hh = getenv("FASTKMER_HT_HUGE"); hh && hh[0]) c->lh_huge_thr = (uint32_t)strtoul(hh, nullptr, 10);
     if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
         c->piece_bytes_set = true;
@@ -614,6 +617,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         c->st_cuts_set = true;
     }
     if (const char *pm = getenv("FASTKMER_PIECE_MODE"); pm && pm[0]) c->piece_mode = atoi(pm);
+    if (const char *xc = getenv("FASTKMER_XCH_CUTS"); xc && xc[0]) c->xch_cuts = atoi(xc);
     if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
     if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
     if (const char *pc = getenv("FASTKMER_PRECOUNT"); pc && pc[0]) c->precount = atoi(pc);
@@ -1923,27 +1927,38 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     FK_TRY(ensure(c->lh_sp[0], (uint64_t)ngroups * 4 + 64));
     if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
     uint64_t *const pin = c->pin_ht.as<uint64_t>();
-    // 128-bit keys: the groups of more than lh_big_thr k-mers take 6144-slot tables (one workgroup
-    // per CU) instead of spilling most of their keys from the 2048-slot ones
-    uint64_t nbig = 0;
+    // 128-bit keys: the groups of more than lh_big_thr k-mers take larger tables instead of spilling
+    // most of their keys from the 2048-slot ones: up to lh_huge_thr k-mers 3072 slots (two 512-thread
+    // workgroups per CU), above it (or above lh_big_thr when lh_huge_thr is 0) 6144 slots (one
+    // 1024-thread workgroup per CU)
+    uint64_t nbig = 0, nmid = 0;
     const uint32_t big_thr = KW == 2 ? c->lh_big_thr : 0u;
+    const uint32_t huge_thr = big_thr && c->lh_huge_thr > big_thr ? c->lh_huge_thr : 0u;
     if (big_thr) {
-        FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 4 + 64));
-        HIP_TRY(launch_ht_big_list(groups, ngroups, big_thr, c->lh_glist.as<uint32_t>(), sp_total + 1, s));
-        HIP_TRY(hipMemcpyAsync(pin, sp_total + 1, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemsetAsync(sp_total + 1, 0, 8, s));
+        FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 8 + 64));
+        uint32_t *const gl = c->lh_glist.as<uint32_t>();
+        HIP_TRY(launch_ht_big_list(groups, ngroups, huge_thr ? huge_thr : big_thr, 0u, gl, sp_total + 1, s));
+        if (huge_thr) HIP_TRY(launch_ht_big_list(groups, ngroups, big_thr, huge_thr, gl + ngroups, sp_total, s));
+        HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
         HIP_TRY(hipStreamSynchronize(s));
-        nbig = pin[0];
+        nbig = pin[1];
+        nmid = huge_thr ? pin[0] : 0;
     }
-    c->stats.ht_big_groups = nbig;
+    c->stats.ht_big_groups = nbig + nmid;
     HIP_TRY(launch_ht_combine(c->W, c->lh_recs.as<uint64_t>(), groups, nullptr, ngroups, c->cfg.k, 0,
                               c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
                               c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe, nullptr, nullptr,
-                              nbig ? big_thr : 0u));
+                              nbig + nmid ? big_thr : 0u));
     if (nbig)
         HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
                                          c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
                                          d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
+    if (nmid)
+        HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>() + ngroups,
+                                         (uint32_t)nmid, c->cfg.k, c->lh_spill[0].as<uint64_t>(),
+                                         c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
+                                         c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, true));
     // the groups that spilled, listed on the device (a parent each: its spill range and count)
     FK_TRY(ensure(c->lh_parents, (uint64_t)ngroups * sizeof(LhItem) + 64));
     HIP_TRY(launch_ht_spill_list(groups, c->lh_sp[0].as<uint32_t>(), ngroups, c->lh_parents.as<LhItem>(),
@@ -2976,11 +2991,20 @@ static double xch_recv_frac(const fk_ctx *c, uint64_t recs) {
 // of the job (every step when its size is unknown), at most STAGE_MAXP - 1 times before fk_finish.
 static int xch_maybe_stage(fk_ctx *c, size_t s1) {
     if (c->st_np >= (uint32_t)STAGE_MAXP - 1 || s1 <= c->segs_counted) return FK_OK;
-    uint64_t recs = 0;
-    for (size_t i = c->segs_counted; i < s1; ++i)
-        for (uint64_t n : c->xch.segs[i].rec) recs += n;
+    uint64_t recs = 0, before = 0;
+    for (size_t i = 0; i < s1; ++i)
+        for (uint64_t n : c->xch.segs[i].rec) (i < c->segs_counted ? before : recs) += n;
     const double frac = xch_recv_frac(c, recs);
-    if (frac > 0.0 && frac < 1.0 / STAGE_MAXP) return FK_OK;
+    // a piece ends once the received records reach the next cut of the job (st_cuts, as the local
+    // path's pieces): the last piece -- expanded after the last byte -- is the smallest.  (Staging at
+    // every quarter left ~30 % of a 6.25 GB rank for fk_finish: 61.7 ms after it against 47.7 for
+    // the local path, profiles/r04c_xch_tail.txt.)
+    if (frac > 0.0 && !c->xch_cuts) {
+        if (frac < 1.0 / STAGE_MAXP) return FK_OK;
+    } else if (frac > 0.0) {
+        if (c->st_np >= (uint32_t)c->st_cuts.size()) return FK_OK;
+        if (xch_recv_frac(c, before + recs) < c->st_cuts[c->st_np]) return FK_OK;
+    }
     const uint32_t np0 = c->st_np;
     FK_TRY(xch_stage_segments(c, s1, frac));
     if (c->st_np > np0) c->npieces += 1;  // (segments without k-mers add no piece)

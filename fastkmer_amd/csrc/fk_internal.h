@@ -314,13 +314,14 @@ hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, 
                              const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys, uint32_t *ocnt,
                              hipStream_t s, int probe = 0, const uint64_t *psrc = nullptr,
                              const uint32_t *sub_off = nullptr, uint32_t big_thr = 0);
-// 128-bit keys: round 1 of the groups of more than big_thr k-mers (k_ht_big_list) in 6144-slot tables
-hipError_t launch_ht_big_list(const LhGroup *groups, uint32_t ngroups, uint32_t thr, uint32_t *glist,
+// 128-bit keys: round 1 of the groups of thr < k-mers <= hi (hi = 0: no bound; k_ht_big_list) in
+// 6144-slot tables, or (mid) 3072-slot ones
+hipError_t launch_ht_big_list(const LhGroup *groups, uint32_t ngroups, uint32_t thr, uint32_t hi, uint32_t *glist,
                               unsigned long long *n_out, hipStream_t s);
 hipError_t launch_ht_combine128_big(const uint64_t *src, const LhGroup *groups, const uint32_t *glist, uint32_t n,
                                     int k, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
                                     const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys,
-                                    uint32_t *ocnt, hipStream_t s);
+                                    uint32_t *ocnt, hipStream_t s, bool mid = false);
 hipError_t launch_ht_gather(int KW, const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb,
                             const uint64_t *okeys, const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt,
                             hipStream_t s);
