@@ -315,6 +315,7 @@ struct fk_ctx {
     int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
     uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG: k > 32, groups of more k-mers take larger tables (0: none)
     uint32_t lh_huge_thr = 0;     // FASTKMER_HT_HUGE: groups up to this many k-mers take 3072 slots, above 6144 (0: all 6144)
+    int64_t lh_big64 = 0;         // FASTKMER_HT_BIG64: k <= 32, groups of more k-mers take 8192-slot tables (0: none, -1: by the distinct ratio; measured slower)
     int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
@@ -598,6 +599,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *sp = getenv("FASTKMER_HT_SUBPART"); sp && sp[0]) c->lh_subpart = atoi(sp);
     if (const char *hb = getenv("FASTKMER_HT_BIG"); hb && hb[0]) c->lh_big_thr = (uint32_t)strtoul(hb, nullptr, 10);
     if (const char *hh = getenv("FASTKMER_HT_HUGE"); hh && hh[0]) c->lh_huge_thr = (uint32_t)strtoul(hh, nullptr, 10);
+    if (const char *h6 = getenv("FASTKMER_HT_BIG64"); h6 && h6[0]) c->lh_big64 = strtoll(h6, nullptr, 10);
     if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
         c->piece_bytes_set = true;
@@ -1931,9 +1933,15 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     // most of their keys from the 2048-slot ones: up to lh_huge_thr k-mers 3072 slots (two 512-thread
     // workgroups per CU), above it (or above lh_big_thr when lh_huge_thr is 0) 6144 slots (one
     // 1024-thread workgroup per CU)
+    // 64-bit keys: groups whose expected distinct keys (k-mers x the last count's distinct ratio)
+    // pass ~3/4 of a 4096-slot table may take 8192 slots (FASTKMER_HT_BIG64: k-mers, -1 auto; default 0:
+    // off -- at k = 28 over a 3 Gbp genome every group overflows, and one 104 KB workgroup per CU
+    // measured 18.9 against 16.7 ms, profiles/r04c_ht5_big64.txt)
     uint64_t nbig = 0, nmid = 0;
-    const uint32_t big_thr = KW == 2 ? c->lh_big_thr : 0u;
-    const uint32_t huge_thr = big_thr && c->lh_huge_thr > big_thr ? c->lh_huge_thr : 0u;
+    const uint32_t thr64 = c->lh_big64 >= 0 ? (uint32_t)c->lh_big64
+                                            : (uint32_t)std::min(4.0e9, 3072.0 / std::max(0.05, c->lh_ratio));
+    const uint32_t big_thr = KW == 2 ? c->lh_big_thr : thr64;
+    const uint32_t huge_thr = KW == 2 && big_thr && c->lh_huge_thr > big_thr ? c->lh_huge_thr : 0u;
     if (big_thr) {
         FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 8 + 64));
         uint32_t *const gl = c->lh_glist.as<uint32_t>();
@@ -1950,10 +1958,14 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
                               c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
                               c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe, nullptr, nullptr,
                               nbig + nmid ? big_thr : 0u));
-    if (nbig)
+    if (nbig && KW == 2)
         HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
                                          c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
                                          d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
+    else if (nbig)
+        HIP_TRY(launch_ht_combine64_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
+                                        c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
+                                        d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
     if (nmid)
         HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>() + ngroups,
                                          (uint32_t)nmid, c->cfg.k, c->lh_spill[0].as<uint64_t>(),

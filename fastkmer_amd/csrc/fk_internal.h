@@ -318,6 +318,11 @@ hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, 
 // 6144-slot tables, or (mid) 3072-slot ones
 hipError_t launch_ht_big_list(const LhGroup *groups, uint32_t ngroups, uint32_t thr, uint32_t hi, uint32_t *glist,
                               unsigned long long *n_out, hipStream_t s);
+// 64-bit keys: round 1 of the listed heavy groups in 8192-slot tables
+hipError_t launch_ht_combine64_big(const uint64_t *src, const LhGroup *groups, const uint32_t *glist, uint32_t n,
+                                   int k, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
+                                   const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys,
+                                   uint32_t *ocnt, hipStream_t s);
 hipError_t launch_ht_combine128_big(const uint64_t *src, const LhGroup *groups, const uint32_t *glist, uint32_t n,
                                     int k, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
                                     const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys,
