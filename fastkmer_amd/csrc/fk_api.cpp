@@ -348,6 +348,9 @@ struct fk_ctx {
     PinBuf pin_ht;                        // hash count: spilled parents down, spill-round items up
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
+    hipStream_t tier_stream = nullptr;    // the block / big tiers, beside the wave tier (FASTKMER_TIER_SIDE)
+    hipEvent_t tier_done = nullptr;       // ... done (the context stream waits for it)
+    int tier_side = 0;                    // FASTKMER_TIER_SIDE=1: measured neutral (count 83.4 vs 83.2-83.5 ms at configs[2]), off
     bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
     // The sorted count's result is bucket-major ("gapped"): bucket q's distinct keys ascending at its
     // first slot buckets[q].begin of res_keys / out_counts, dense_off[q] = their exclusive offset in the
@@ -620,6 +623,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     }
     if (const char *pm = getenv("FASTKMER_PIECE_MODE"); pm && pm[0]) c->piece_mode = atoi(pm);
     if (const char *xc = getenv("FASTKMER_XCH_CUTS"); xc && xc[0]) c->xch_cuts = atoi(xc);
+    if (const char *ts = getenv("FASTKMER_TIER_SIDE"); ts && ts[0]) c->tier_side = atoi(ts);
     if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
     if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
     if (const char *pc = getenv("FASTKMER_PRECOUNT"); pc && pc[0]) c->precount = atoi(pc);
@@ -676,6 +680,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         }
     }
     e = hipEventCreateWithFlags(&c->tier_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->tier_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->tier_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         fk_destroy(c);
         return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
@@ -722,6 +728,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->file_pin[0].release();
     c->file_pin[1].release();
     if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
+    if (c->tier_done) (void)hipEventDestroy(c->tier_done);
+    if (c->tier_stream) (void)hipStreamDestroy(c->tier_stream);
     release(c->xsend);
     release(c->xrecv);
     for (fk_ctx::PieceRes *r : {&c->acc, &c->acc2, &c->tmp})
@@ -1724,11 +1732,19 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         htrace("sorted: tiers read");
         c->stats.block_buckets = ntier[0];
         c->stats.big_buckets = ntier[1];
+        // the block / big tiers (disjoint buckets, their own counters) on a side stream beside the
+        // wave tier, so they fill the CUs the wave tier's tail leaves
+        hipStream_t ts = s;
+        const bool side = c->tier_side && c->tier_stream && (ntier[0] || ntier[1]);
+        if (side) {
+            ts = c->tier_stream;
+            HIP_TRY(hipStreamWaitEvent(ts, c->tier_ev, 0));
+        }
         if (ntier[0] && c->KW == 1) {
             HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k,
                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                           B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
-                                          cap, 99, lists, s));
+                                          cap, 99, lists, ts));
         } else if (ntier[0]) {
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
             // 768-slot table (a cell of a large bin, ~340 keys at configs[3]'s per-GPU bins), the rest
@@ -1736,11 +1752,11 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             if (c->mid_tier)
                 HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                         okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                        B.bucket_unique->as<uint64_t>(), s));
+                                                        B.bucket_unique->as<uint64_t>(), ts));
             HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), ntier[0], k,
                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                        B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
-                                       lists, s, c->mid_tier ? WAVE128_MID_CAP : 0u));
+                                       lists, ts, c->mid_tier ? WAVE128_MID_CAP : 0u));
         }
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
@@ -1748,16 +1764,20 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), ntier[1], k,
                                               okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                               B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
-                                              lists + nbuckets, s));
-            HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
+                                              lists + nbuckets, ts));
+            HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, ts));
+            HIP_TRY(hipStreamSynchronize(ts));
         }
         if (nlarge) {
             FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
             HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), ntier[1], k,
                                              c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                              B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                             lists + nbuckets, s));
+                                             lists + nbuckets, ts));
+        }
+        if (side) {
+            HIP_TRY(hipEventRecord(c->tier_done, ts));
+            HIP_TRY(hipStreamWaitEvent(s, c->tier_done, 0));
         }
         c->stats.oversize_buckets = nlarge;
     } else {
