@@ -315,6 +315,7 @@ struct fk_ctx {
     int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
     uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG: k > 32, groups of more k-mers take larger tables (0: none)
     uint32_t lh_huge_thr = 0;     // FASTKMER_HT_HUGE: groups up to this many k-mers take 3072 slots, above 6144 (0: all 6144)
+    double lh_load = 0.5;         // FASTKMER_HT_LOAD: expected distinct keys per group / table slots
     int64_t lh_big64 = 0;         // FASTKMER_HT_BIG64: k <= 32, groups of more k-mers take 8192-slot tables (0: none, -1: by the distinct ratio; measured slower)
     int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
@@ -603,6 +604,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *hb = getenv("FASTKMER_HT_BIG"); hb && hb[0]) c->lh_big_thr = (uint32_t)strtoul(hb, nullptr, 10);
     if (const char *hh = getenv("FASTKMER_HT_HUGE"); hh && hh[0]) c->lh_huge_thr = (uint32_t)strtoul(hh, nullptr, 10);
     if (const char *h6 = getenv("FASTKMER_HT_BIG64"); h6 && h6[0]) c->lh_big64 = strtoll(h6, nullptr, 10);
+    if (const char *hl = getenv("FASTKMER_HT_LOAD"); hl && hl[0]) c->lh_load = std::min(1.0, std::max(0.05, atof(hl)));
     if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
         c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
         c->piece_bytes_set = true;
@@ -1898,7 +1900,7 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     hipStream_t s = c->stream;
     const uint32_t nlb = c->nlb, nchunks = (uint32_t)chunks.size();
     const uint32_t KW = (uint32_t)c->KW;
-    const double per_group = KW == 1 ? 4096.0 * 0.5 : 2048.0 * 0.5;  // LH_TS / LH2_TS slots, half full
+    const double per_group = (KW == 1 ? 4096.0 : 2048.0) * c->lh_load;  // LH_TS / LH2_TS slots, half full
     std::vector<uint8_t> flog(nlb, 0);
     std::vector<uint32_t> gbase(nlb + 1, 0);
     std::vector<uint64_t> rec_base(nlb + 1, 0), km_base(nlb + 1, 0);
