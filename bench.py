@@ -1,13 +1,15 @@
 """Benchmark: exact canonical k-mer counting throughput on MI355X.
 
 Metric (BASELINE.json): input bases/sec for the whole node, k=28 short reads,
-1/2/4/8 GPUs, counts bit-exact.  Workloads (synthetic ">r%010d" 100 bp reads,
-0.2% substitutions, 0.05% N):
-  * N = 1 (default c2): BASELINE configs[1], k=28 m=10 x=3 B=2048, 1 GB of
-    FASTA from a 100 Mbp virtual genome;
-  * N > 1 (default c3): BASELINE configs[2], k=28 m=10 x=3 B=8192, 6.25 GB of
-    FASTA per GPU from a 3 Gbp virtual genome (N = 8: the 50 GB job),
-    weak scaling.
+1/2/4/8 GPUs, counts bit-exact.  Synthetic ">r%010d" 100 bp reads, 0.2%
+substitutions, 0.05% N.
+
+`value` is weak-scaled: every rank runs the same per-GPU job at every N, so
+the driver's 1 -> N ratio compares like with like.  The default job is
+BASELINE configs[1]'s: k=28 m=10 x=3 B=2048, 1 GB of FASTA per GPU from a
+100 Mbp virtual genome (--workload picks another).  Beside it the line carries
+`configs2_per_gpu`: configs[2]'s per-GPU load, k=28 m=10 x=3 B=8192, 6.25 GB
+per GPU from a 3 Gbp virtual genome (at N = 8: the 50 GB job), also at every N.
 
 One step = one job over the rank's shard (SparkBinKmerCounter.executeJob,
 SBKC:989-1046): parse + 2-bit encode + signature + super-k-mer records in one
@@ -23,15 +25,18 @@ fused kernel mapping every landed tile meanwhile, and with N > 1 every landed
 piece exchanged while the next one is copied) and ends with the counts on the
 device.  `device_resident_value` is the same job with the FASTA already in HBM;
 the roofline of the fused encode+signature kernel comes from that leg (HIP
-events around its one launch, on the stream it runs on).  With N > 1, or more
-than 2 GB per GPU, that leg runs only with --device-leg (a rank's 6.25 GB shard
-would otherwise hold both legs' buffers on its GPU at once).
+events around its one launch, on the stream it runs on).  That leg runs at
+N = 1 and <= 2 GB per GPU unless --device-leg asks for it.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
-        (N > 1: torchrun --nproc-per-node N bench.py --gpus N ...; one process per GPU,
-         the RCCL unique id travels over torch.distributed's gloo group)
-        python bench.py --rehearse-local N --bytes-per-gpu B   (N ranks as threads of one
-         process on one GPU: the whole native N > 1 path with the in-process transport)
+          N > 1 without a launcher: bench.py starts N worker processes itself (one per GPU,
+          RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 in their environment) before any
+          GPU call, and fails if fewer than N GPUs are visible; --dry-run prints that plan.
+        torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+          (one process per GPU; --gpus must equal WORLD_SIZE; the RCCL unique id travels over
+          torch.distributed's gloo group)
+        python bench.py --rehearse-local N [--bytes-per-gpu B]   (N ranks as threads of one
+          process on one GPU: the whole native N > 1 path with the in-process transport)
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -39,6 +44,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -144,17 +151,17 @@ def load_traffic(kernel: str):
 
 
 class Rank:
-    """One rank's context and its shard (pinned host copy and device copy)."""
+    """One rank's context and its shard (pinned host copy and, for the HBM-resident leg, a device copy)."""
 
-    def __init__(self, args, wl, rank: int, world: int, device: int):
+    def __init__(self, wl: str, nbytes: int, use_ht: bool, device_leg: bool, rank: int, world: int, device: int):
         k, m, B, read_len, genome, seq_type, _, _ = WORKLOADS[wl]
         self.k, self.m, self.B, self.read_len, self.genome, self.seq_type = k, m, B, read_len, genome, seq_type
         self.rank, self.world, self.device = rank, world, device
         self.dev = torch.device("cuda", device)
-        self.kc = fk.KmerCounter(k, m, 3, B, use_ht=args.use_ht, sequence_type=seq_type, n_ranks=world, rank=rank,
+        self.kc = fk.KmerCounter(k, m, 3, B, use_ht=use_ht, sequence_type=seq_type, n_ranks=world, rank=rank,
                                  device=device)
         if seq_type == 1:
-            n_bases = args.bytes_per_gpu * 60 // 61
+            n_bases = nbytes * 60 // 61
             data = long_sequence_fasta(n_bases, seed=SEED + rank)
             self.fasta_bytes, self.bases = len(data), n_bases
             import numpy as np
@@ -164,7 +171,7 @@ class Rank:
             self.dev_in = self.host.to(self.dev)
         else:
             rec_bytes = read_len + 14
-            n_reads = args.bytes_per_gpu // rec_bytes
+            n_reads = nbytes // rec_bytes
             self.fasta_bytes, self.bases = n_reads * rec_bytes, n_reads * read_len
             self.dev_in = torch.empty(self.fasta_bytes, dtype=torch.uint8, device=self.dev)
             with torch.cuda.device(self.dev):
@@ -173,7 +180,7 @@ class Rank:
             self.host = torch.empty(self.fasta_bytes, dtype=torch.uint8, pin_memory=True)
             self.host.copy_(self.dev_in)
         torch.cuda.synchronize(self.dev)
-        if args.no_device_leg:  # the HBM-resident copy only feeds that leg
+        if not device_leg:  # the HBM-resident copy only feeds that leg
             self.dev_in = None
             torch.cuda.empty_cache()
 
@@ -184,6 +191,10 @@ class Rank:
     def step_device(self):
         self.kc.ingest_device(self.dev_in.data_ptr(), self.fasta_bytes)
         self.kc.finish()
+
+    def close(self):
+        self.kc.close()
+        self.host = self.dev_in = None
 
 
 def exchange_figures(st: dict, world: int) -> dict:
@@ -198,9 +209,218 @@ def exchange_figures(st: dict, world: int) -> dict:
     return out
 
 
+
+class Topology:
+    """Where this process sits: one rank of a torch.distributed job (one process per GPU, RCCL
+    between them), the only rank, or --rehearse-local N ranks as threads on GPU 0."""
+
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.local = args.rehearse_local
+        self.distributed = self.world > 1
+        self.n_ranks = self.local or self.world
+
+    def barrier_sync(self):
+        torch.cuda.synchronize()
+        if self.distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(self, v: float) -> float:
+        if not self.distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def make_ranks(topo: Topology, wl: str, nbytes: int, use_ht: bool, device_leg: bool) -> list:
+    if topo.local:
+        ranks = [Rank(wl, nbytes, use_ht, device_leg, r, topo.local, 0) for r in range(topo.local)]
+        fk.comm_init_local([r.kc for r in ranks])
+        return ranks
+    ranks = [Rank(wl, nbytes, use_ht, device_leg, topo.rank, topo.world, topo.local_rank)]
+    if topo.distributed:
+        uid = [fk.comm_unique_id() if topo.rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ranks[0].kc.comm_init(uid[0])
+    return ranks
+
+
+def run_step(ranks: list, step_name: str) -> None:
+    if len(ranks) == 1:
+        getattr(ranks[0], step_name)()
+        return
+    errs = [None] * len(ranks)
+
+    def work(i):
+        try:
+            getattr(ranks[i], step_name)()
+        except Exception as e:  # noqa: BLE001
+            errs[i] = e
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(ranks))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+def timed(topo: Topology, ranks: list, step_name: str, steps: int, warmup: int):
+    """W untimed steps, then exactly K steps between barrier + synchronize pairs; the max over ranks."""
+    for _ in range(warmup):
+        run_step(ranks, step_name)
+    topo.barrier_sync()
+    per, t0 = [], time.perf_counter()
+    for _ in range(steps):
+        run_step(ranks, step_name)
+        per.append([r.kc.stats() for r in ranks])
+    topo.barrier_sync()
+    return topo.max_over_ranks(time.perf_counter() - t0), per
+
+
+def run_leg(args, topo: Topology, wl: str, nbytes: int, device_leg: bool) -> dict:
+    """One workload: the headline leg (pinned-host FASTA -> counts on the device) and, if asked, the
+    HBM-resident leg with the encode+signature kernel's roofline.  Collective over the ranks."""
+    ranks = make_ranks(topo, wl, nbytes, args.use_ht, device_leg)
+    elapsed, host_stats = timed(topo, ranks, "step_host", args.steps, args.warmup)
+    res = {"wl": wl, "elapsed": elapsed, "hs": host_stats[-1][0], "fasta_bytes": ranks[0].fasta_bytes,
+           "bases_per_gpu": ranks[0].bases,
+           "bases_all": sum(r.bases for r in ranks) * (topo.world if topo.distributed else 1),
+           "transport": ranks[0].kc.comm_transport}
+    if os.environ.get("FASTKMER_BENCH_MEMINFO"):  # device memory left after the host-input leg
+        free_b, total_b = torch.cuda.mem_get_info()
+        st0 = host_stats[-1][0]
+        print(f"meminfo [{wl}]: {free_b / 1e9:.1f} GB free of {total_b / 1e9:.1f} GB after the host-input leg; "
+              f"buckets {st0['buckets']}, oversize {st0['oversize_buckets']}, fine bits {st0['fine_bits']}",
+              file=sys.stderr, flush=True)
+    host_sizes = [r.kc.bin_sizes() for r in ranks]
+    for i, s in enumerate(host_sizes):
+        assert int(s.sum()) == host_stats[-1][i]["distinct"] > 0
+    if device_leg:
+        dev_elapsed, dev_stats = timed(topo, ranks, "step_device", args.steps, args.warmup)
+        for r, s in zip(ranks, host_sizes):  # size-independent self-check: both legs counted the same shard
+            assert (r.kc.bin_sizes() == s).all()
+        res.update(dev_elapsed=dev_elapsed, dev_stats=dev_stats)
+    for r in ranks:
+        r.close()
+    del ranks
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
+def leg_line(args, topo: Topology, res: dict) -> dict:
+    """The figures of one leg as they appear in the JSON line."""
+    wl, hs = res["wl"], res["hs"]
+    k, m, B, read_len, genome, seq_type, _, _ = WORKLOADS[wl]
+    n = topo.n_ranks
+    par = (f"bins round-robin (bin % {n}) over {n} GPUs, records exchanged by the library "
+           f"({res['transport']} transport)" if n > 1 else "one GPU")
+    if topo.local:
+        par += f" -- REHEARSAL: {topo.local} ranks as threads on one GPU"
+    out = {
+        "value": res["bases_all"] * args.steps / res["elapsed"],
+        "unit": "bases/s",
+        "ms_per_step": res["elapsed"] / args.steps * 1e3,
+        "config": {"workload": workload_label(wl, res["fasta_bytes"]), "k": k, "m": m, "x": 3, "B": B,
+                   "useHT": int(args.use_ht), "sequenceType": seq_type, "fasta_bytes_per_gpu": res["fasta_bytes"],
+                   "bases_per_gpu": res["bases_per_gpu"],
+                   "parallelism": par},
+        "stages_ms": {"h2d": hs["ms_h2d"], "map_overlapped_with_h2d": hs["ms_signature"],
+                      "partition": hs["ms_partition"], "count": hs["ms_count"]},
+        "pcie_h2d_GBps": res["fasta_bytes"] / (hs["ms_h2d"] * 1e-3) / 1e9 if hs["ms_h2d"] else None,
+        "kmers_per_gpu": hs["kmers"], "distinct_rank0": hs["distinct"],
+        "buckets_rank0": {"all": hs["buckets"], "above_wave_tier": hs["block_buckets"],
+                          "above_2048_keys": hs["big_buckets"], "large_path": hs["oversize_buckets"],
+                          "cell_bits": hs["fine_bits"]},
+    }
+    if n > 1:
+        out["exchange"] = exchange_figures(hs, n)
+    return out
+
+
+def roofline(args, topo: Topology, res: dict) -> dict:
+    """The encode+signature kernel: algorithmic bytes = FASTA bytes read per launch,
+    time = the fused kernel's HIP-event duration on the stream it runs on (HBM-resident leg)."""
+    dev_stats = res["dev_stats"]
+    fused = all(s[0]["fused_map"] for s in dev_stats)
+    t_k = sum(s[0]["ms_signature_kernel"] + s[0]["ms_encode_kernel"] for s in dev_stats) / len(dev_stats) * 1e-3
+    kname = "k_map_fused" if fused else "k_fasta_parse + k_superkmers"
+    achieved = res["fasta_bytes"] / t_k
+    return {"bound": "hbm", "kernel": kname + " (encode + signature: FASTA bytes -> records)",
+            "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+            "traffic": load_traffic(kname) if res["fasta_bytes"] == 999_999_906 else None,
+            "bytes_alg_per_launch": res["fasta_bytes"], "ms_per_launch": t_k * 1e3,
+            "measured": "HIP events around each launch on the context's map stream (HBM-resident leg)",
+            "note": "priced against HBM for the contract; the measured limiter is VALU issue (DESIGN.md 4)"}
+
+
+# ---------------------------------------------------------------------------
+# --gpus N without a launcher: one worker process per GPU, started before any GPU call
+# ---------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv: list) -> int:
+    """`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment): starts N copies of this
+    script as ranks 0..N-1 of one torch.distributed job on this node (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT), the same environment torchrun gives them.  This process never
+    touches the GPU (it only counts the devices); it waits for the workers and exits with the first
+    failing worker's code, stopping the others."""
+    n = args.gpus
+    port = _free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv
+    envs = []
+    for r in range(n):
+        e = dict(os.environ)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                 HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        envs.append(e)
+    visible = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+    if args.dry_run:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                "HSA_ENABLE_IPC_MODE_LEGACY")
+        print(json.dumps({"launcher": "bench.py", "world_size": n, "visible_gpus": visible, "argv": cmd,
+                          "ranks": [{k: e[k] for k in keys} for e in envs]}), flush=True)
+        return 0
+    if visible < n:
+        print(f"bench.py --gpus {n}: only {visible} GPU(s) visible; an N-GPU run needs N GPUs of one node "
+              f"(one rank per GPU)", file=sys.stderr, flush=True)
+        return 2
+    procs = [subprocess.Popen(cmd, env=e) for e in envs]
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (one rank each).  Without WORLD_SIZE in the environment, N > 1 "
+                         "starts the N ranks itself; under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--bytes-per-gpu", type=int, default=0, help="FASTA bytes per GPU (0: the workload's)")
@@ -212,126 +432,63 @@ def main() -> None:
                          "only; a 6.25 GB shard would hold both legs' buffers on its GPU at once)")
     ap.add_argument("--use-ht", action="store_true", help="hash count (extractKXmersHT, useHT=1)")
     ap.add_argument("--workload", default="", choices=["", "c2", "c3", "c4", "c5"],
-                    help="c2 = BASELINE configs[1] (default at N = 1); c3 = configs[2] (default at N > 1); "
-                         "c4 = configs[3] (k=55 m=12, two-word keys); c5 = configs[4] shape (one long record)")
+                    help="the `value` workload at every N: c2 = BASELINE configs[1]'s per-GPU job (default); "
+                         "c3 = configs[2]'s per-GPU load; c4 = configs[3] (k=55 m=12, two-word keys); "
+                         "c5 = configs[4] shape (one long record)")
+    ap.add_argument("--c3-leg", default="auto", choices=["auto", "on", "off"],
+                    help="also run configs[2]'s per-GPU load (6.25 GB, B=8192; the 8-GPU 50 GB job at N = 8) "
+                         "and report it as `configs2_per_gpu` (auto: on unless the value workload is c3 or "
+                         "this is a --rehearse-local run)")
     ap.add_argument("--rehearse-local", type=int, default=0,
                     help="N ranks as threads of this process on GPU 0 (in-process transport), a rehearsal "
                          "of the N-GPU job on one card")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="with --gpus N > 1: print the ranks' launch plan as JSON and exit (no GPU use)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    local = args.rehearse_local
-    if local and world > 1:
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1 and not args.rehearse_local:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.gpus is not None and args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    topo = Topology(args)
+    if args.gpus is not None and not args.rehearse_local and args.gpus != topo.world:
+        print(f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={topo.world}: the two must agree",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if topo.local and topo.world > 1:
         raise SystemExit("--rehearse-local runs in one process")
-    n_ranks = local or world
-    wl = args.workload or ("c2" if n_ranks == 1 else "c3")
-    if not args.bytes_per_gpu:
-        args.bytes_per_gpu = WORKLOADS[wl][6]
+    if args.dry_run:
+        raise SystemExit("--dry-run needs --gpus N > 1 without a launcher")
+    wl = args.workload or "c2"
+    nbytes = args.bytes_per_gpu or WORKLOADS[wl][6]
     # the roofline leg is the N = 1 line's, at its 1 GB; a 6.25 GB shard (configs[2] / [3] per GPU)
     # would hold both legs' buffers on its GPU at once (k = 55: ~57 GB per k-mer array)
-    if (n_ranks > 1 or args.bytes_per_gpu > 2_000_000_000) and not args.device_leg:
-        args.no_device_leg = True
-    distributed = world > 1
-    torch.cuda.set_device(0 if local else local_rank)
-    if distributed:
+    device_leg = not args.no_device_leg and (args.device_leg or (topo.n_ranks == 1 and nbytes <= 2_000_000_000))
+    c3_leg = args.c3_leg == "on" or (args.c3_leg == "auto" and wl != "c3" and not topo.local)
+    torch.cuda.set_device(0 if topo.local else topo.local_rank)
+    if topo.distributed:
         dist.init_process_group("gloo")  # bootstrap + host barriers; the records move over RCCL in the library
 
-    if local:
-        ranks = [Rank(args, wl, r, local, 0) for r in range(local)]
-        fk.comm_init_local([r.kc for r in ranks])
-    else:
-        ranks = [Rank(args, wl, rank, world, local_rank)]
-        if distributed:
-            uid = [fk.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            ranks[0].kc.comm_init(uid[0])
+    res = run_leg(args, topo, wl, nbytes, device_leg)
+    res3 = run_leg(args, topo, "c3", WORKLOADS["c3"][6], False) if c3_leg else None
 
-    def run(step_name):
-        if len(ranks) == 1:
-            getattr(ranks[0], step_name)()
-            return
-        errs = [None] * len(ranks)
-
-        def work(i):
-            try:
-                getattr(ranks[i], step_name)()
-            except Exception as e:  # noqa: BLE001
-                errs[i] = e
-        th = [threading.Thread(target=work, args=(i,)) for i in range(len(ranks))]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        for e in errs:
-            if e is not None:
-                raise e
-
-    def barrier_sync():
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    def max_over_ranks(v: float) -> float:
-        if not distributed:
-            return v
-        t = torch.tensor([v], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def timed(step_name, steps, warmup):
-        for _ in range(warmup):
-            run(step_name)
-        barrier_sync()
-        per, t0 = [], time.perf_counter()
-        for _ in range(steps):
-            run(step_name)
-            per.append([r.kc.stats() for r in ranks])
-        barrier_sync()
-        return max_over_ranks(time.perf_counter() - t0), per
-
-    # leg 1 (SURVEY 8d's timer, the headline): FASTA in pinned host memory -> counts on the device
-    elapsed, host_stats = timed("step_host", args.steps, args.warmup)
-    if os.environ.get("FASTKMER_BENCH_MEMINFO"):  # device memory left after the host-input leg
-        free_b, total_b = torch.cuda.mem_get_info()
-        st0 = host_stats[-1][0]
-        print(f"meminfo: {free_b / 1e9:.1f} GB free of {total_b / 1e9:.1f} GB after the host-input leg; "
-              f"buckets {st0['buckets']}, oversize {st0['oversize_buckets']}, fine bits {st0['fine_bits']}",
-              file=sys.stderr, flush=True)
-    host_sizes = [r.kc.bin_sizes() for r in ranks]
-    for r, s in zip(ranks, host_sizes):
-        assert int(s.sum()) == host_stats[-1][ranks.index(r)]["distinct"] > 0
-    # leg 2: FASTA resident in HBM; the encode+signature kernel's roofline
-    dev_elapsed, dev_stats = None, None
-    if not args.no_device_leg:
-        dev_elapsed, dev_stats = timed("step_device", args.steps, args.warmup)
-        for r, s in zip(ranks, host_sizes):  # size-independent self-check: both legs counted the same shard
-            assert (r.kc.bin_sizes() == s).all()
-
-    if rank == 0:
-        r0 = ranks[0]
-        k, m, B, read_len, genome, seq_type, _, desc = WORKLOADS[wl]
-        bases_all = sum(r.bases for r in ranks) * (world if distributed else 1)
-        hs = host_stats[-1][0]
+    if topo.rank == 0:
+        k, m, B, read_len, genome, seq_type, _, _ = WORKLOADS[wl]
         metric = "input bases/sec (whole node), k=28 short reads, 1/2/4/8 GPUs"
         if wl not in ("c2", "c3"):
             metric += f" [{wl} workload, not the headline configuration]"
         if args.use_ht:
             metric += " [useHT=1: hash count]"
-        par = (f"bins round-robin (bin % {n_ranks}) over {n_ranks} GPUs, records exchanged by the library "
-               f"({r0.kc.comm_transport} transport)" if n_ranks > 1 else "one GPU")
-        if local:
-            par += f" -- REHEARSAL: {local} ranks as threads on one GPU"
+        line = leg_line(args, topo, res)
         out = {
             "metric": metric,
-            "value": bases_all * args.steps / elapsed,
-            "unit": "bases/s",
-            "n_gpus": 1 if local else world,
+            "value": line.pop("value"),
+            "unit": line.pop("unit"),
+            "n_gpus": 1 if topo.local else topo.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": line.pop("ms_per_step"),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -342,48 +499,25 @@ def main() -> None:
             "timed_region": "FASTA in pinned host memory -> H2D (segments on a copy stream, the fused map on every "
                             "landed tile; N > 1: every landed piece exchanged over RCCL while the next is copied) -> "
                             "count -> counts resident on the device (write=0)",
-            "config": {"workload": workload_label(wl, r0.fasta_bytes), "k": k, "m": m, "x": 3, "B": B, "useHT": int(args.use_ht),
-                       "sequenceType": seq_type, "fasta_bytes_per_gpu": r0.fasta_bytes, "bases_per_gpu": r0.bases,
-                       "parallelism": par},
-            "stages_ms": {"h2d": hs["ms_h2d"], "map_overlapped_with_h2d": hs["ms_signature"],
-                          "partition": hs["ms_partition"], "count": hs["ms_count"]},
-            "pcie_h2d_GBps": r0.fasta_bytes / (hs["ms_h2d"] * 1e-3) / 1e9 if hs["ms_h2d"] else None,
-            "kmers_per_gpu": hs["kmers"], "distinct_rank0": hs["distinct"],
-            "buckets_rank0": {"all": hs["buckets"], "above_wave_tier": hs["block_buckets"], "above_2048_keys": hs["big_buckets"],
-                              "large_path": hs["oversize_buckets"], "cell_bits": hs["fine_bits"]},
+            "weak_scaling_unit": "the same per-GPU job at every N (config.workload); value = all ranks' bases / "
+                                 "the slowest rank's time",
         }
-        if n_ranks > 1:
-            out["exchange"] = exchange_figures(hs, n_ranks)
-        if dev_stats is not None:
-            ds = dev_stats[-1][0]
-            out["device_resident_value"] = bases_all * args.steps / dev_elapsed
-            out["device_resident_ms_per_step"] = dev_elapsed / args.steps * 1e3
+        out.update(line)
+        if "dev_stats" in res:
+            ds = res["dev_stats"][-1][0]
+            out["device_resident_value"] = res["bases_all"] * args.steps / res["dev_elapsed"]
+            out["device_resident_ms_per_step"] = res["dev_elapsed"] / args.steps * 1e3
             out["device_resident_stages_ms"] = {"map": ds["ms_signature"] + ds["ms_parse"],
                                                 "partition": ds["ms_partition"], "count": ds["ms_count"]}
-            if n_ranks > 1:
-                out["device_resident_exchange"] = exchange_figures(ds, n_ranks)
-            fused = all(s[0]["fused_map"] for s in dev_stats)
-            # encode+signature stage: algorithmic bytes = FASTA bytes read per launch,
-            # time = the fused kernel's HIP-event duration on its stream (two kernels when not fused)
-            t_k = sum(s[0]["ms_signature_kernel"] + s[0]["ms_encode_kernel"] for s in dev_stats) / len(dev_stats) * 1e-3
-            kname = ("k_map_fused" if fused else "k_fasta_parse + k_superkmers")
-            achieved = r0.fasta_bytes / t_k
-            out["roofline"] = {"bound": "hbm", "kernel": kname + " (encode + signature: FASTA bytes -> records)",
-                               "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                               "frac": achieved / HBM_PEAK,
-                               "traffic": load_traffic(kname) if r0.fasta_bytes == 999_999_906 else None,
-                               "bytes_alg_per_launch": r0.fasta_bytes, "ms_per_launch": t_k * 1e3,
-                               "measured": "HIP events around each launch on the context's map stream "
-                                           "(HBM-resident leg)",
-                               "note": "priced against HBM for the contract; the measured limiter is VALU "
-                                       "issue (about 6.5e8 wave64 VALU instructions per GB at about 3.7 "
-                                       "cycles each per SIMD, profiles/r04b_pmc_split_map.txt)"}
-        if n_ranks == 1 and not args.no_cpu_baseline and wl == "c2":
+            if topo.n_ranks > 1:
+                out["device_resident_exchange"] = exchange_figures(ds, topo.n_ranks)
+            out["roofline"] = roofline(args, topo, res)
+        if res3 is not None:
+            out["configs2_per_gpu"] = leg_line(args, topo, res3)
+        if topo.n_ranks == 1 and not args.no_cpu_baseline and wl == "c2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_bytes, k, m, B, read_len, genome)
         print(json.dumps(out), flush=True)
-    for r in ranks:
-        r.kc.close()
-    if distributed:
+    if topo.distributed:
         dist.destroy_process_group()
 
 

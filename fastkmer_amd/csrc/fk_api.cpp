@@ -194,10 +194,15 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// FASTKMER_HOST_TRACE=1: host timestamps of the count's steps on stderr (where the GPU waits on the host)
+// -DFK_PROBES library, FASTKMER_HOST_TRACE=1: host timestamps of the count's steps on stderr (where
+// the GPU waits on the host)
 static void htrace(const char *what) {
+#ifdef FK_PROBES
     static const bool on = getenv("FASTKMER_HOST_TRACE") && getenv("FASTKMER_HOST_TRACE")[0] == '1';
     if (on) fprintf(stderr, "htrace %.3f %s\n", now_ms(), what);
+#else
+    (void)what;
+#endif
 }
 
 // Every exported call that touches the GPU selects the context's device for
@@ -224,6 +229,7 @@ struct DeviceGuard {
     DeviceGuard &operator=(const DeviceGuard &) = delete;
 };
 
+constexpr int FUSED_NT = 512;  // threads per fused map workgroup (256-thread tiles measured 2.5 vs 1.1 ms per GB)
 constexpr uint32_t CHUNK_RECORDS = 16384;  // records per expansion workgroup (never spans two bins)
 
 // The sorted count's shape: cell bits F (super-cells of 2^F2 cells), tiers.
@@ -251,25 +257,15 @@ struct fk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS: route every bucket through 5b
-    uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: cap/4)
-    int scatter_wc = 1;        // FASTKMER_DEBUG_SCATTER: 0 plain scatter; 2, 3 timing probes (wrong results)
-    int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early (timing only)
-    int expand_levels = 2;     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 super-cells then cells
+    // Test hooks (result-preserving; they steer inputs that FASTA data cannot aim at onto a path):
+    bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS=1: route every bucket through the streaming path
+    uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: auto)
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
-    int x2_l2 = 0;             // FASTKMER_X2_L2: level-2 workgroup size (128, 256, 512; 0 = by keys per super-cell)
-    uint32_t greedy_cap = 0;   // FASTKMER_GREEDY_CAP (probe): pack cells into buckets of up to this many keys (0 = wave_cap)
-    uint32_t wave_cap = WAVE_BUCKET_CAP;  // FASTKMER_WAVE_CAP: keys per wave-tier bucket (128, 256, 512)
-    uint32_t wave_slots = 768;  // FASTKMER_WAVE_SLOTS: table slots of a 512-key wave bucket (768 or 1024;
-                                // 128-bit keys: 384 or 512 per 256-key bucket alike)
-    int hist_bin = 1;          // FASTKMER_HIST_BIN: 1 bin-resident super-cell histogram, 0 one workgroup per chunk
-    int f2_bits = -1;          // FASTKMER_F2: cells per super-cell = 2^f2_bits (two-level expansion; -1 = auto)
-    int wave_bpw = 2;          // FASTKMER_WAVE_BPW: buckets per wave in the wave tier (1, 2, 4; 2 measured fastest)
-    bool parse_scan = true;    // FASTKMER_PARSE_LOOKBACK=1: always parse with the line look-back
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
-    int fused_probe = 0;       // FASTKMER_FUSED_PROBE: stop the fused map kernel after a phase (timing only)
-    int fused_nt = 512;        // FASTKMER_FUSED_NT: threads per fused map workgroup (256 or 512)
-    int split_map = 0;         // FASTKMER_SPLIT_MAP=1: the map as a parse kernel + a signature-pass kernel (measurement)
+    // Measurement-only (a library built with -DFK_PROBES; wrong results by design):
+    int dbg_phase = 99;        // FASTKMER_DEBUG_PHASE: stop the bucket kernel early
+    int fused_probe = 0;       // FASTKMER_FUSED_PROBE: stop the fused map kernel after a phase
+    int split_map = 0;         // FASTKMER_SPLIT_MAP=1: the map as a parse kernel + a signature-pass kernel
     bool last_map_fused = false;  // the last fk_map used the fused kernel (stats, tests)
     // grouped emit (fk_set_grouped_emit): send buffer grouped by (destination, local bin)
     bool grouped = false;
@@ -277,8 +273,6 @@ struct fk_ctx {
     DevBuf grp_table;                        // bin -> dest * grp_nlb + bin / n_ranks
     std::vector<uint64_t> grp_rec, grp_kmer; // per part, after fk_map
     const uint64_t *rsrc = nullptr;          // records the count stage reads (precs, or d_recv when grouped)
-    int count_mode = 1;        // FASTKMER_COUNT_MODE (k <= 32): 0 one workgroup per bucket of <= 2048 keys,
-                               // 1 tiered (wave kernel for buckets <= WAVE_BUCKET_CAP, block kernel, large path)
 
     // input
     // host ingest: bytes are streamed to fasta_own (appended until the next fk_map)
@@ -311,13 +305,8 @@ struct fk_ctx {
     DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
     DevBuf lh_parents, lh_parents2, lh_plan, lh_suboff, lh_part, lh_glist;  // spill rounds: parents, their plan, sub-ranges
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
-    int lh_mode = 1;              // FASTKMER_LDS_HT: 1 = LDS tables for useHT (k <= 32), 0 = global tables
-    int lh_subpart = 1;           // FASTKMER_HT_SUBPART=0: spill sub-items filter the whole parent range
-    uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG: k > 32, groups of more k-mers take larger tables (0: none)
-    uint32_t lh_huge_thr = 0;     // FASTKMER_HT_HUGE: groups up to this many k-mers take 3072 slots, above 6144 (0: all 6144)
-    double lh_load = 0.5;         // FASTKMER_HT_LOAD: expected distinct keys per group / table slots
-    int64_t lh_big64 = 0;         // FASTKMER_HT_BIG64: k <= 32, groups of more k-mers take 8192-slot tables (0: none, -1: by the distinct ratio; measured slower)
-    int lh_probe = 0;             // FASTKMER_LH_PROBE: stop the combine kernel after a phase (timing only)
+    uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG (test hook): k > 32, groups of more k-mers take 6144-slot tables
+    int lh_probe = 0;             // FASTKMER_LH_PROBE (-DFK_PROBES): stop the combine kernel after a phase
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
     uint64_t nrec = 0, nkmers = 0;
@@ -344,20 +333,17 @@ struct fk_ctx {
     double ms_h2d = 0.0;  // last fk_ingest: first copy issued -> last copy done
     bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
-    PinBuf pin_up, pin_down, pin_merge;  // staging: chunk tables up, per-bin counts down, merge tables up
+    PinBuf pin_up, pin_down;              // staging: chunk tables up, per-bin counts down
     PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
     PinBuf pin_ht;                        // hash count: spilled parents down, spill-round items up
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
-    hipStream_t tier_stream = nullptr;    // the block / big tiers, beside the wave tier (FASTKMER_TIER_SIDE)
-    hipEvent_t tier_done = nullptr;       // ... done (the context stream waits for it)
-    int tier_side = 0;                    // FASTKMER_TIER_SIDE=1: measured neutral (count 83.4 vs 83.2-83.5 ms at configs[2]), off
     bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
     // The sorted count's result is bucket-major ("gapped"): bucket q's distinct keys ascending at its
     // first slot buckets[q].begin of res_keys / out_counts, dense_off[q] = their exclusive offset in the
     // bin-ordered result, bin_off / h_bin_off per bin.  Readers gather a bin's buckets (fk_get_bin) or
-    // the whole result (fk_write_bins); the pieces merged by count_piece need dense arrays (want_dense).
-    bool gapped = false, dense_ready = false, want_dense = false;
+    // the whole result (fk_write_bins).
+    bool gapped = false, dense_ready = false;
     // The LDS hash count's result stays in the bins' regions: local bin lb's distinct entries at
     // h_ht_kbase[lb] of lh_okeys / lh_ocnt (no packing pass; fk_write_bins packs it once).
     bool ht_regions = false;
@@ -372,53 +358,21 @@ struct fk_ctx {
     // is emitted in pieces grouped by (destination, local bin) and each piece is exchanged
     // while the next one is still being copied in; fk_finish sends the last piece, then
     // counts every received segment (the reduceByKey shuffle of SBKC:1034-1042)
-    // per-piece counts (sorted count): pieces are counted while later ones are still being copied
-    // in (or received), fk_finish counts the last one and merges the pieces' results (fk_merge.inc)
-    struct PieceRes {
-        DevBuf keys, counts, bin_off;
-        std::vector<uint64_t> h_bin_off;
-        uint64_t distinct = 0;
-    };
-    PieceRes acc, acc2, tmp;      // running result of the counted pieces, merge target, the newest piece
-    uint32_t npieces = 0;         // pieces counted into acc in the current job
-    bool pieces_void = false;     // a fallback or a retract: the pieces are counted again at the end
-    bool count_pieces = true;     // FASTKMER_PIECE_COUNT=0: count the whole input in fk_finish
-    uint64_t tiles_counted = 0;   // one rank: tiled records [0, tiles_counted) counted
+    // staged pieces (one rank, or the received segments with a communicator; sorted count, k <= 63):
+    // each piece of the input is partitioned and expanded into its own key array while later pieces
+    // land; the job's buckets are counted once over every piece's keys (no per-piece count, no merge)
+    bool pieces_void = false;     // a fallback or a retract: the job is counted whole at the end
+    uint64_t tiles_counted = 0;   // one rank: tiled records [0, tiles_counted) staged
     uint64_t job_bytes = 0;       // one rank: the job's input size when one fk_ingest call holds it all, or
                                   // announced by fk_ingest_reserve (0: unknown)
     uint64_t reserve_bytes = 0;   // fk_ingest_reserve's size for the next job
-    std::vector<double> piece_cuts{0.55};  // FASTKMER_PIECE_CUTS: piece ends as fractions of job_bytes
-    double job_ratio = -1.0;      // distinct / k-mers of the last one-rank job (-1: none yet)
-    size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) counted
-    double acc_ms_part = 0.0, acc_ms_count = 0.0, acc_ms_merge = 0.0;  // the job's earlier pieces
-    DevBuf m2_bin_tile0, m2_split_a, m2_split_b, m2_bnd, m2_tcount, m2_toff, m2_keys, m2_counts;
-    // staged pieces (one rank, sorted count, k <= 32; FASTKMER_PIECE_MODE=1, the default): each
-    // piece is partitioned and expanded into its own key array while later pieces land; the job's
-    // buckets are counted once over every piece's keys (no per-piece count, no merge)
-    int piece_mode = 1;                          // FASTKMER_PIECE_MODE: 1 staged, 0 count + merge per piece
+    size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) staged
     std::vector<double> st_cuts{0.4, 0.7, 0.9};  // piece ends of a staged job (FASTKMER_PIECE_CUTS; 45 / 70 / 85 % measured 22.84 vs 22.77 ms)
-    bool st_cuts_set = false;
-    int xch_cuts = 1;  // FASTKMER_XCH_CUTS=0: the exchange path stages every quarter of the job (round 3)
-    double st_one_level = 0.0;                   // FASTKMER_STAGED_ONE_LEVEL: one-pass expansion below this job fraction
     uint32_t st_np = 0;                          // pieces expanded in the current job
+    uint32_t st_cut = 0;                         // one rank: st_cuts passed in the current job
     SortedPlan st_plan;                          // the job's cells (fixed by its first piece)
     uint64_t st_kmers = 0;                       // k-mers expanded so far
     DevBuf st_keys[STAGE_MAXP], st_cb[STAGE_MAXP], st_total, piece_starts;
-    int st_starts = 1;                           // FASTKMER_STAGED_STARTS=0: the wave tier reads st_cb itself
-    // pre-count (k <= 32, one rank, staged): once pre_at pieces are expanded, their buckets are counted
-    // while the rest lands; the final count merges those results with the later pieces' raw keys
-    // (FASTKMER_PRECOUNT: 1 always, 0 (default) never, -1 when the last job was redundant; measured at
-    // configs[1]: 23.14 ms per step against 22.97 without -- the final count's cost is per bucket
-    // (table clears, ranks), not per key, so merging fewer entries saves little)
-    int precount = 0;
-    int mid_tier = 1;  // FASTKMER_MID128=0: 128-bit buckets above the wave tier go to the radix sort
-    uint32_t pre_at = 2;
-    bool pre_done = false;
-    uint32_t pre_np = 0;
-    uint64_t pre_nb = 0, pre_kmers = 0;
-    DevBuf pre_total, pre_base, pre_flags, pre_flag_scan, pre_buckets, pre_unique, pre_tier_list, pre_piece_starts,
-        pre_keys, pre_counts;
-    hipEvent_t pre_ev[2] = {nullptr, nullptr};
     hipEvent_t st_ev[4 * STAGE_MAXP] = {};       // per piece: partition begin / end, expansion begin / end
 
     fk::Comm *comm = nullptr;
@@ -557,85 +511,40 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->W = cfg->k <= 32 ? 2 : 3;
     c->KW = cfg->k <= 32 ? 1 : 2;
     c->fm = make_fastmod((uint32_t)c->Bc);
-    const char *dbg = getenv("FASTKMER_DEBUG_LARGE_BUCKETS");
-    c->force_large = dbg && dbg[0] == '1';
-    const char *ct = getenv("FASTKMER_DEBUG_CELL_TARGET");
-    c->cell_target = ct ? (uint32_t)atoi(ct) : 0u;
-    // Result-altering timing probes (a kernel stopped after a phase, a scatter that drops keys)
-    // exist only in a library built with -DFK_PROBES (python -m fastkmer_amd.build --probes); the
-    // product library reads none of them.  FASTKMER_DEBUG_SCATTER=0 (the plain scatter, exact)
-    // stays available everywhere.
-    const char *sc = getenv("FASTKMER_DEBUG_SCATTER");
-    if (sc && sc[0] && atoi(sc) == 0) c->scatter_wc = 0;
-#ifdef FK_PROBES
-    if (sc && sc[0]) c->scatter_wc = atoi(sc);
-    const char *ph = getenv("FASTKMER_DEBUG_PHASE");
-    if (ph && ph[0]) c->dbg_phase = atoi(ph);
-#endif
-    if (const char *x1 = getenv("FASTKMER_X2_L1"); x1 && x1[0]) c->x2_l1 = atoi(x1);
-    if (const char *x2 = getenv("FASTKMER_X2_L2"); x2 && x2[0]) c->x2_l2 = atoi(x2);
-    const char *el = getenv("FASTKMER_EXPAND_LEVELS");
-    if (el && el[0]) c->expand_levels = atoi(el);
-    const char *wc = getenv("FASTKMER_WAVE_CAP");
-    if (wc && wc[0]) c->wave_cap = (uint32_t)atoi(wc);
-    if (const char *ws = getenv("FASTKMER_WAVE_SLOTS"); ws && ws[0]) c->wave_slots = (uint32_t)atoi(ws);
-    if (const char *gc = getenv("FASTKMER_GREEDY_CAP"); gc && gc[0]) c->greedy_cap = (uint32_t)atoi(gc);
-    const char *f2 = getenv("FASTKMER_F2");
-    if (const char *hb = getenv("FASTKMER_HIST_BIN"); hb && hb[0]) c->hist_bin = atoi(hb);
-    if (f2 && f2[0]) c->f2_bits = std::max(0, std::min(9, atoi(f2)));
-    const char *bp = getenv("FASTKMER_WAVE_BPW");
-    if (bp && bp[0]) c->wave_bpw = atoi(bp);
-    const char *pl = getenv("FASTKMER_PARSE_LOOKBACK");
-    if (pl && pl[0]) c->parse_scan = atoi(pl) == 0;
-    const char *fu = getenv("FASTKMER_FUSED");
-    if (fu && fu[0]) c->fused = atoi(fu);
-    const char *fn = getenv("FASTKMER_FUSED_NT");
-    if (fn && fn[0]) c->fused_nt = atoi(fn) == 256 ? 256 : 512;
-#ifdef FK_PROBES
-    const char *fp = getenv("FASTKMER_FUSED_PROBE");
-    if (fp && fp[0]) c->fused_probe = atoi(fp);
-    if (const char *sm = getenv("FASTKMER_SPLIT_MAP"); sm && sm[0]) c->split_map = atoi(sm);
-    const char *lp = getenv("FASTKMER_LH_PROBE");
-    if (lp && lp[0]) c->lh_probe = atoi(lp);
-#endif
-    const char *lh = getenv("FASTKMER_LDS_HT");
-    if (lh && lh[0]) c->lh_mode = atoi(lh);
-    if (const char *sp = getenv("FASTKMER_HT_SUBPART"); sp && sp[0]) c->lh_subpart = atoi(sp);
-    if (const char *hb = getenv("FASTKMER_HT_BIG"); hb && hb[0]) c->lh_big_thr = (uint32_t)strtoul(hb, nullptr, 10);
-    if (const char *hh = getenv("FASTKMER_HT_HUGE"); hh && hh[0]) c->lh_huge_thr = (uint32_t)strtoul(hh, nullptr, 10);
-    if (const char *h6 = getenv("FASTKMER_HT_BIG64"); h6 && h6[0]) c->lh_big64 = strtoll(h6, nullptr, 10);
-    if (const char *hl = getenv("FASTKMER_HT_LOAD"); hl && hl[0]) c->lh_load = std::min(1.0, std::max(0.05, atof(hl)));
-    if (const char *pb = getenv("FASTKMER_PIECE_BYTES"); pb && pb[0]) {
-        c->piece_bytes = std::max(1ull << 16, strtoull(pb, nullptr, 10));
+    // The product library reads eight variables: three sizes of the streamed input and five test
+    // hooks that steer small inputs onto paths only large or adversarial inputs reach (all
+    // result-preserving).  Timing probes that alter results exist only in a library built with
+    // -DFK_PROBES (python -m fastkmer_amd.build --probes).
+    auto env = [](const char *name) -> const char * {
+        const char *v = getenv(name);
+        return v && v[0] ? v : nullptr;
+    };
+    if (const char *v = env("FASTKMER_PIECE_BYTES")) {  // piece size of a streamed job (1 GB with a communicator)
+        c->piece_bytes = std::max(1ull << 16, strtoull(v, nullptr, 10));
         c->piece_bytes_set = true;
     }
-    if (const char *pc = getenv("FASTKMER_PIECE_COUNT"); pc && pc[0]) c->count_pieces = atoi(pc) != 0;
-    if (const char *pc = getenv("FASTKMER_PIECE_CUTS"); pc && pc[0]) {  // e.g. "0.6" or "0.5,0.8"
-        c->piece_cuts.clear();
-        for (const char *q = pc; *q;) {
+    if (const char *v = env("FASTKMER_PIECE_CUTS")) {  // staged piece ends as job fractions, e.g. "0.4,0.7,0.9"
+        c->st_cuts.clear();
+        for (const char *q = v; *q;) {
             char *e = nullptr;
             const double f = strtod(q, &e);
             if (e == q) break;
-            if (f > 0.0 && f < 1.0) c->piece_cuts.push_back(f);
+            if (f > 0.0 && f < 1.0 && c->st_cuts.size() < STAGE_MAXP - 1) c->st_cuts.push_back(f);
             q = *e == ',' ? e + 1 : e;
         }
-        c->st_cuts = c->piece_cuts;
-        if (c->st_cuts.size() > STAGE_MAXP - 1) c->st_cuts.resize(STAGE_MAXP - 1);
-        c->st_cuts_set = true;
     }
-    if (const char *pm = getenv("FASTKMER_PIECE_MODE"); pm && pm[0]) c->piece_mode = atoi(pm);
-    if (const char *xc = getenv("FASTKMER_XCH_CUTS"); xc && xc[0]) c->xch_cuts = atoi(xc);
-    if (const char *ts = getenv("FASTKMER_TIER_SIDE"); ts && ts[0]) c->tier_side = atoi(ts);
-    if (const char *ol = getenv("FASTKMER_STAGED_ONE_LEVEL"); ol && ol[0]) c->st_one_level = atof(ol);
-    if (const char *ss = getenv("FASTKMER_STAGED_STARTS"); ss && ss[0]) c->st_starts = atoi(ss);
-    if (const char *pc = getenv("FASTKMER_PRECOUNT"); pc && pc[0]) c->precount = atoi(pc);
-    if (const char *m1 = getenv("FASTKMER_MID128"); m1 && m1[0]) c->mid_tier = atoi(m1);
-    if (const char *pa = getenv("FASTKMER_PRECOUNT_AT"); pa && pa[0])
-        c->pre_at = (uint32_t)std::max(1, std::min(STAGE_MAXP - 1, atoi(pa)));
-    if (const char *sg = getenv("FASTKMER_INGEST_SEG"); sg && sg[0])
-        c->ingest_seg = std::max(1ull << 16, strtoull(sg, nullptr, 10));
-    const char *cm = getenv("FASTKMER_COUNT_MODE");
-    if (cm && cm[0]) c->count_mode = atoi(cm);
+    if (const char *v = env("FASTKMER_INGEST_SEG")) c->ingest_seg = std::max(1ull << 16, strtoull(v, nullptr, 10));
+    if (const char *v = env("FASTKMER_DEBUG_LARGE_BUCKETS")) c->force_large = v[0] == '1';
+    if (const char *v = env("FASTKMER_DEBUG_CELL_TARGET")) c->cell_target = (uint32_t)atoi(v);
+    if (const char *v = env("FASTKMER_X2_L1")) c->x2_l1 = atoi(v);
+    if (const char *v = env("FASTKMER_FUSED")) c->fused = atoi(v);
+    if (const char *v = env("FASTKMER_HT_BIG")) c->lh_big_thr = (uint32_t)strtoul(v, nullptr, 10);
+#ifdef FK_PROBES
+    if (const char *v = env("FASTKMER_DEBUG_PHASE")) c->dbg_phase = atoi(v);
+    if (const char *v = env("FASTKMER_FUSED_PROBE")) c->fused_probe = atoi(v);
+    if (const char *v = env("FASTKMER_SPLIT_MAP")) c->split_map = atoi(v);
+    if (const char *v = env("FASTKMER_LH_PROBE")) c->lh_probe = atoi(v);
+#endif
     if (cfg->device >= 0) {
         if (cfg->device >= ndev) {
             delete c;
@@ -674,16 +583,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
             return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
         }
     }
-    for (auto &ev : c->pre_ev) {
-        e = hipEventCreate(&ev);
-        if (e != hipSuccess) {
-            fk_destroy(c);
-            return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
-        }
-    }
     e = hipEventCreateWithFlags(&c->tier_ev, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->tier_done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->tier_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         fk_destroy(c);
         return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
@@ -724,21 +624,13 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->comm = nullptr;
     c->pin_up.release();
     c->pin_down.release();
-    c->pin_merge.release();
     c->pin_tier.release();
     c->pin_ht.release();
     c->file_pin[0].release();
     c->file_pin[1].release();
     if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
-    if (c->tier_done) (void)hipEventDestroy(c->tier_done);
-    if (c->tier_stream) (void)hipStreamDestroy(c->tier_stream);
     release(c->xsend);
     release(c->xrecv);
-    for (fk_ctx::PieceRes *r : {&c->acc, &c->acc2, &c->tmp})
-        for (DevBuf *b : {&r->keys, &r->counts, &r->bin_off}) release(*b);
-    for (DevBuf *b : {&c->m2_bin_tile0, &c->m2_split_a, &c->m2_split_b, &c->m2_bnd, &c->m2_tcount,
-                      &c->m2_toff, &c->m2_keys, &c->m2_counts})
-        release(*b);
     for (auto &e : c->xev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : c->seg_evs)
@@ -758,11 +650,6 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     for (int p = 0; p < STAGE_MAXP; ++p) release(c->st_keys[p]), release(c->st_cb[p]);
     release(c->st_total);
     release(c->piece_starts);
-    for (DevBuf *b : {&c->pre_total, &c->pre_base, &c->pre_flags, &c->pre_flag_scan, &c->pre_buckets, &c->pre_unique,
-                      &c->pre_tier_list, &c->pre_piece_starts, &c->pre_keys, &c->pre_counts})
-        release(*b);
-    for (auto &ev : c->pre_ev)
-        if (ev) (void)hipEventDestroy(ev);
     if (c->seg_ev) (void)hipEventDestroy(c->seg_ev);
     for (auto &ev : c->h2d_ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -830,7 +717,7 @@ static bool premap_eligible(const fk_ctx *c) {
 // kernel's waves keep the SIMDs busy), or the fused kernel (FASTKMER_SPLIT_MAP=0, the 256-thread
 // tiles, probes).  map_vslots is sized by the callers (map_vslots_reserve).
 constexpr uint64_t MAP_VSLOT_TILES = 32768;  // ~1.07 GB of FASTA per split launch pair (140 MB of slots)
-static bool map_split(const fk_ctx *c) { return c->split_map && c->fused_nt == 512 && !c->fused_probe; }
+static bool map_split(const fk_ctx *c) { return c->split_map && !c->fused_probe; }
 static int map_vslots_reserve(fk_ctx *c, uint64_t ntiles) {
     if (!map_split(c)) return FK_OK;
     return ensure(c->map_vslots, std::min(ntiles, MAP_VSLOT_TILES) * map_fused_vslot() * 4);
@@ -839,7 +726,7 @@ static int map_launch(fk_ctx *c, const uint8_t *fa, uint64_t n, int more, uint64
     const uint64_t cap = map_split(c) ? c->map_vslots.bytes / ((uint64_t)map_fused_vslot() * 4) : 0;
     for (uint64_t b = 0; b < nt;) {
         const uint64_t m = cap ? std::min(cap, nt - b) : nt - b;
-        HIP_TRY(launch_map_fused(c->fused_nt, c->cfg.k, c->cfg.m, fa, n, more, t0 + b, m, c->fm,
+        HIP_TRY(launch_map_fused(FUSED_NT, c->cfg.k, c->cfg.m, fa, n, more, t0 + b, m, c->fm,
                                  c->rec_hdr.as<uint32_t>(), c->rec_pos.as<uint16_t>(), c->rec_code.as<uint32_t>(),
                                  c->tcnt.as<uint32_t>(), c->tstat.as<uint32_t>(), c->counters.as<unsigned long long>(),
                                  s, c->fused_probe, cap ? c->map_vslots.as<uint32_t>() : nullptr));
@@ -849,7 +736,7 @@ static int map_launch(fk_ctx *c, const uint8_t *fa, uint64_t n, int more, uint64
 }
 
 static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
-    const uint64_t tile = fm_tile_bytes(c->fused_nt), span = fm_span_bytes(c->fused_nt);
+    const uint64_t tile = fm_tile_bytes(FUSED_NT), span = fm_span_bytes(FUSED_NT);
     const uint64_t end = final_ ? (landed + tile - 1) / tile : (landed >= span ? (landed - span) / tile + 1 : 0);
     if (end <= c->pm_tiles) return FK_OK;
     if (c->tcnt.bytes < end * 4 || c->tstat.bytes < end * 8 || c->rec_hdr.bytes < end * map_fused_tcap() * 4 ||
@@ -914,7 +801,7 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     c->d_fasta = c->fasta_own.as<uint8_t>();
     if (c->pm_active) {
         // record slots and per-tile counts of every tile this input can hold (kept on growth)
-        const uint64_t tiles = (need + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
+        const uint64_t tiles = (need + fm_tile_bytes(FUSED_NT) - 1) / fm_tile_bytes(FUSED_NT) + 1;
         if (c->tcnt.bytes < tiles * 4) FK_TRY(grow_keep(c->tcnt, tiles * 4, c->tcnt.bytes, s));
         if (c->tstat.bytes < tiles * 8) FK_TRY(grow_keep(c->tstat, tiles * 8, c->tstat.bytes, s));
         const uint64_t hdr_need = tiles * map_fused_tcap() * 4, pos_need = tiles * map_fused_tcap() * 2;
@@ -1024,7 +911,7 @@ static int reserve_impl(fk_ctx *c, uint64_t total_bytes) {
     FK_TRY(ensure(c->fasta_own, total_bytes));
     c->reserve_bytes = total_bytes;  // the next (streamed) job's size: piece cuts and staged plans follow it
     if (premap_eligible(c)) {
-        const uint64_t tiles = (total_bytes + fm_tile_bytes(c->fused_nt) - 1) / fm_tile_bytes(c->fused_nt) + 1;
+        const uint64_t tiles = (total_bytes + fm_tile_bytes(FUSED_NT) - 1) / fm_tile_bytes(FUSED_NT) + 1;
         FK_TRY(ensure(c->rec_hdr, tiles * map_fused_tcap() * 4));
         FK_TRY(ensure(c->rec_pos, tiles * map_fused_tcap() * 2));
         FK_TRY(ensure(c->rec_code, tiles * map_fused_cslot() * 4));
@@ -1074,8 +961,18 @@ FK_EXPORT int fk_split_bytes(const char *path, int32_t world, int32_t rank, int3
     return FK_OK;
 }
 
+// With a communicator the split is the job's: (world, rank) must be the context's own (a mismatch
+// would count some byte ranges twice and skip others while the exchange still completes).
+static int check_split_rank(const fk_ctx *c, int32_t world, int32_t rank, const char *what) {
+    if (c->comm && (world != (int32_t)c->G || rank != c->cfg.rank))
+        return set_err(FK_E_INVALID, "%s: split %d of %d on the context of rank %d of %u", what, rank, world,
+                       c->cfg.rank, c->G);
+    return FK_OK;
+}
+
 static int ingest_file_impl(fk_ctx *c, const char *path, int32_t world, int32_t rank, uint64_t window) {
     if (!path) return set_err(FK_E_INVALID, "null path");
+    FK_TRY(check_split_rank(c, world, rank, "fk_ingest_file_range"));
     if (!c->ingest_fresh && c->d_fasta) return set_err(FK_E_STATE, "fk_ingest_file_range inside a streamed input");
     Fd f;
     uint64_t size = 0;
@@ -1194,7 +1091,7 @@ static int32_t global_bin(const fk_ctx *c, uint32_t lb) {
 static int map_fused(fk_ctx *c, uint64_t n, bool *ok) {
     hipStream_t s = c->stream;
     *ok = false;
-    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    const uint64_t tile = fm_tile_bytes(FUSED_NT);
     const uint64_t ntiles = (n + tile - 1) / tile;
     FK_TRY(ensure(c->tcnt, ntiles * 4));
     FK_TRY(ensure(c->tstat, ntiles * 8));
@@ -1325,7 +1222,7 @@ static int map_records(fk_ctx *c) {
     };
     c->last_map_fused = fused_ok;
     c->stats.fused_map = fused_ok ? 1 : 0;
-    bool parse_scan = c->parse_scan;
+    bool parse_scan = true;  // the scan variant first; the look-back rerun if it flags the input
     if (!fused_ok) FK_TRY(run_parse(parse_scan));
 
     // 2. signature + super-k-mer records (retried once if the capacity estimate was short)
@@ -1377,6 +1274,27 @@ static int map_records(fk_ctx *c) {
     return FK_OK;
 }
 
+// Grouped emit: records and k-mers of the mapped records per (destination, local bin) part and the
+// send counts per destination, under the current group table (the receiver needs no partition pass).
+static int grouped_part_counts(fk_ctx *c) {
+    hipStream_t s = c->stream;
+    const uint32_t nparts = c->G * c->grp_nlb;
+    c->grp_rec.assign(nparts, 0);
+    c->grp_kmer.assign(nparts, 0);
+    c->send_counts.assign(c->G, 0);
+    if (c->nrec) {
+        FK_TRY(part_count(c->dest, map_src(c), 0, c->G, c->grp_table.as<uint32_t>(), nparts, c->ws, s));
+        HIP_TRY(hipMemcpyAsync(c->grp_rec.data(), c->dest.rec.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->grp_kmer.data(), c->dest.kmer.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    for (uint32_t d = 0; d < c->G; ++d)
+        for (uint32_t lb = 0; lb < c->grp_nlb; ++lb) c->send_counts[d] += c->grp_rec[(uint64_t)d * c->grp_nlb + lb];
+    return FK_OK;
+}
+
+static int build_group_table(fk_ctx *c);
+
 FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     DeviceGuard dg_(c->device);
@@ -1387,18 +1305,7 @@ FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     // 3a. destination histogram (records per rank)
     c->send_counts.assign(c->G, 0);
     if (c->grouped) {
-        // parts = (destination, local bin): the receiver needs no partition pass
-        const uint32_t nparts = c->G * c->grp_nlb;
-        c->grp_rec.assign(nparts, 0);
-        c->grp_kmer.assign(nparts, 0);
-        if (c->nrec) {
-            FK_TRY(part_count(c->dest, map_src(c), 0, c->G, c->grp_table.as<uint32_t>(), nparts, c->ws, s));
-            HIP_TRY(hipMemcpyAsync(c->grp_rec.data(), c->dest.rec.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(c->grp_kmer.data(), c->dest.kmer.p, (uint64_t)nparts * 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
-        }
-        for (uint32_t d = 0; d < c->G; ++d)
-            for (uint32_t lb = 0; lb < c->grp_nlb; ++lb) c->send_counts[d] += c->grp_rec[(uint64_t)d * c->grp_nlb + lb];
+        FK_TRY(grouped_part_counts(c));
     } else if (c->G == 1) {
         c->send_counts[0] = c->nrec;
     } else if (c->nrec) {
@@ -1503,7 +1410,8 @@ FK_EXPORT int fk_set_bin_owners(fk_ctx *c, const int32_t *owner, uint64_t *send_
     c->custom_owners = true;
     c->have_result = false;
     if (c->grouped) {  // the (owner, local bin) parts of the grouped emit follow the new owners
-        FK_TRY(fk_set_grouped_emit(c, 1));
+        FK_TRY(build_group_table(c));
+        if (c->mapped) FK_TRY(grouped_part_counts(c));  // ... and so do the mapped records' parts
     } else if (c->mapped) {  // the destinations of the mapped records changed
         c->send_counts.assign(c->G, 0);
         if (c->G == 1) {
@@ -1538,8 +1446,9 @@ static SortedPlan sorted_plan(const fk_ctx *c, uint64_t max_bin_kmers) {
     // written as whole lines)
     // (two-level expansion: cap / 8, measured faster; the wave tier then holds
     // nearly every cell)
-    const bool tiered = (c->KW == 1 || c->cfg.k <= 63) && c->count_mode == 1 && c->dbg_phase == 99 && !c->force_large;
-    const bool two_level = (c->W == 2 || c->cfg.k <= 63) && c->expand_levels >= 2;
+    // k = 64 (no spare bit in a 128-bit key's hi word): one-level scatter, one workgroup per bucket
+    const bool tiered = c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
+    const bool two_level = c->cfg.k <= 63;
     const uint64_t target = c->cell_target ? c->cell_target
                                            : (c->KW == 2 && tiered ? WAVE128_BUCKET_CAP / 2 : two_level ? cap / 8 : cap / 4);
     int F = 1;
@@ -1548,8 +1457,8 @@ static SortedPlan sorted_plan(const fk_ctx *c, uint64_t max_bin_kmers) {
     F = std::min(F, 2 * k);
     // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
     // cells per super-cell: 2^5 up to F = 13, 2^6 above (measured at configs[1] and at 8x larger bins)
-    const uint32_t wave_cap = c->KW == 1 ? c->wave_cap : WAVE128_BUCKET_CAP;
-    const int F2 = std::min(F, c->f2_bits >= 0 ? c->f2_bits : std::max(5, std::min(6, F - 8))), F1 = F - F2;
+    const uint32_t wave_cap = c->KW == 1 ? WAVE_BUCKET_CAP : WAVE128_BUCKET_CAP;
+    const int F2 = std::min(F, std::max(5, std::min(6, F - 8))), F1 = F - F2;
     pl.F = F, pl.F2 = F2, pl.F1 = F1, pl.tiered = tiered, pl.two_level = two_level, pl.cap = cap, pl.wave_cap = wave_cap;
     pl.max_bin = max_bin_kmers;
     return pl;
@@ -1581,7 +1490,7 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
         constexpr double HIST_PIECES = 1024.0;
         std::vector<uint32_t> pieces, first;
         bool split = false;
-        if (c->hist_bin && nchunks && c->h_bcb.size() == (size_t)c->nlb + 1) {
+        if (nchunks && c->h_bcb.size() == (size_t)c->nlb + 1) {
             for (uint32_t lb = 0; lb < c->nlb; ++lb) {
                 const uint32_t cb = c->h_bcb[lb], ce = c->h_bcb[lb + 1], nc = ce - cb;
                 const uint32_t P = std::max(1u, std::min(nc, (uint32_t)(HIST_PIECES * nc / nchunks + 0.5)));
@@ -1593,7 +1502,7 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
                 split |= P > 1;
             }
         }
-        if (c->hist_bin && split) {
+        if (split) {
             const uint32_t np = (uint32_t)first.size();
             FK_TRY(ensure(c->hpieces, (uint64_t)np * 16));
             FK_TRY(ensure(c->hpiece_first, (uint64_t)np * 4));
@@ -1606,15 +1515,9 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
                                               c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(),
                                               c->hpiece_tot.as<uint32_t>(), s));
             HIP_TRY(hipStreamSynchronize(s));  // the host piece tables are released below
-        } else if (c->hist_bin) {
+        } else {
             HIP_TRY(launch_expand_hist_bin(c->KW, c->rsrc, c->chunks.as<Chunk>(), c->bin_chunk_begin.as<uint32_t>(),
                                            c->nlb, k, F, F2, c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
-        } else {
-            HIP_TRY(hipMemsetAsync(c->cell_total.p, 0, ncell_all * 8, s));
-            HIP_TRY(launch_expand_hist_sc(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F, F2,
-                                          c->cell_total.as<uint64_t>(), c->lp.as<uint32_t>(), s));
-            HIP_TRY(launch_cell_prefix(c->bin_chunk_begin.as<uint32_t>(), c->nlb, F1, c->lp.as<uint32_t>(),
-                                       c->sc_total.as<uint64_t>(), s));
         }
     } else {
         FK_TRY(ensure(c->lp, (uint64_t)nchunks * ncell * 4));
@@ -1624,28 +1527,14 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
                                    c->cell_total.as<uint64_t>(), s));
     }
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), cell_base, ncell_all, cell_base + ncell_all, c->ws, s));
-    if (getenv("FASTKMER_DEBUG_CELL_SIZES")) {  // key-weighted histogram of log2(cell size), stderr
-        std::vector<uint64_t> ct(ncell_all);
-        HIP_TRY(hipMemcpyAsync(ct.data(), c->cell_total.p, ncell_all * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        uint64_t hk[64] = {0}, hc[64] = {0};
-        for (uint64_t v : ct) {
-            const int l = v ? 64 - __builtin_clzll(v) : 0;
-            hk[l] += v;
-            hc[l] += 1;
-        }
-        for (int l = 0; l < 40; ++l)
-            if (hc[l]) fprintf(stderr, "cells <2^%d: %llu cells %llu keys\n", l, (unsigned long long)hc[l], (unsigned long long)hk[l]);
-    }
     if (two_level) {
         FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
         HIP_TRY(launch_expand_two_level(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
                                         F2, c->lp.as<uint32_t>(), cell_base, c->mid.as<uint64_t>(),
-                                        keys.as<uint64_t>(), s, c->x2_l1, total_kmers, c->x2_l2));
+                                        keys.as<uint64_t>(), s, c->x2_l1, total_kmers));
     } else {
         HIP_TRY(launch_expand_scatter(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, k, F,
-                                      c->lp.as<uint32_t>(), cell_base, keys.as<uint64_t>(),
-                                      pl.max_bin < (1ull << 31) ? c->scatter_wc : 0, s));
+                                      c->lp.as<uint32_t>(), cell_base, keys.as<uint64_t>(), s));
     }
     return FK_OK;
 }
@@ -1680,9 +1569,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(cell_total, c->nlb, F,
-                                           c->greedy_cap ? c->greedy_cap : wave_cap, -1,
-                                           B.flags->as<uint32_t>(), s));
+        HIP_TRY(launch_bucket_flags_greedy(cell_total, c->nlb, F, wave_cap, -1, B.flags->as<uint32_t>(), s));
     else
         HIP_TRY(launch_bucket_flags(cell_base, cell_total, c->nlb, F, cap / 4, cap - cap / 4, B.flags->as<uint32_t>(), s));
     HIP_TRY(scan_excl_sum_u32_to_u64(B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), ncell_all,
@@ -1698,7 +1585,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     HIP_TRY(launch_bucket_write(cell_base, B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), c->nlb, F, nbuckets,
                                 total_kmers, B.buckets->as<Bucket>(), s));
     BucketSrc src = src_in;
-    if (src.np > 0 && c->st_starts) {  // the staged pieces' starts per bucket, read by the wave tier
+    if (src.np > 0) {  // the staged pieces' starts per bucket, read by the wave tier
         FK_TRY(ensure(*B.piece_starts, nbuckets * sizeof(PieceStarts)));
         HIP_TRY(launch_bucket_pieces(src, B.buckets->as<Bucket>(), nbuckets, B.piece_starts->as<PieceStarts>(), s));
         src.starts = B.piece_starts->as<PieceStarts>();
@@ -1722,26 +1609,17 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
                                                okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                               B.bucket_unique->as<uint64_t>(), c->wave_bpw, c->wave_cap, c->wave_slots,
-                                               nullptr, s));
+                                               B.bucket_unique->as<uint64_t>(), nullptr, s));
         else
             HIP_TRY(launch_bucket_count128_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
                                                 okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                B.bucket_unique->as<uint64_t>(), c->wave_slots < 2 * WAVE_BUCKET_CAP,
-                                                s));
+                                                B.bucket_unique->as<uint64_t>(), s));
         HIP_TRY(hipEventSynchronize(c->tier_ev));
         uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
         htrace("sorted: tiers read");
         c->stats.block_buckets = ntier[0];
         c->stats.big_buckets = ntier[1];
-        // the block / big tiers (disjoint buckets, their own counters) on a side stream beside the
-        // wave tier, so they fill the CUs the wave tier's tail leaves
         hipStream_t ts = s;
-        const bool side = c->tier_side && c->tier_stream && (ntier[0] || ntier[1]);
-        if (side) {
-            ts = c->tier_stream;
-            HIP_TRY(hipStreamWaitEvent(ts, c->tier_ev, 0));
-        }
         if (ntier[0] && c->KW == 1) {
             HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k,
                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
@@ -1751,14 +1629,13 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
             // 768-slot table (a cell of a large bin, ~340 keys at configs[3]'s per-GPU bins), the rest
             // the LDS radix sort
-            if (c->mid_tier)
-                HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
-                                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                        B.bucket_unique->as<uint64_t>(), ts));
+            HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                    okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                    B.bucket_unique->as<uint64_t>(), ts));
             HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), ntier[0], k,
                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                        B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
-                                       lists, ts, c->mid_tier ? WAVE128_MID_CAP : 0u));
+                                       lists, ts, WAVE128_MID_CAP));
         }
         uint64_t nlarge = ntier[1];
         if (ntier[1] && c->KW == 1 && !c->force_large) {
@@ -1776,10 +1653,6 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                              c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                              B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
                                              lists + nbuckets, ts));
-        }
-        if (side) {
-            HIP_TRY(hipEventRecord(c->tier_done, ts));
-            HIP_TRY(hipStreamWaitEvent(s, c->tier_done, 0));
         }
         c->stats.oversize_buckets = nlarge;
     } else {
@@ -1811,58 +1684,24 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
 }
 
 // The count's result from its buckets: dense_off = the exclusive scan of the distinct keys per bucket,
-// bin_off per local bin (`flag_scan` of the bucket cut: a bin's first cell starts a bucket); kept
-// bucket-major unless want_dense (then compacted into dense_keys / dense_counts).
-static int sorted_result(fk_ctx *c, int F, uint64_t nbuckets, uint64_t total_kmers, DevBuf &okb, CountBufs B) {
+// bin_off per local bin (`flag_scan` of the bucket cut: a bin's first cell starts a bucket).  The
+// result stays bucket-major (no compaction pass): readers gather a bin's buckets (fk_get_bin) or the
+// whole result (fk_write_bins, materialize_dense).
+static int sorted_result(fk_ctx *c, int F, uint64_t nbuckets, DevBuf &okb, CountBufs B) {
     hipStream_t s = c->stream;
     FK_TRY(ensure(c->dense_off, (nbuckets + 1) * 8));
     HIP_TRY(scan_excl_sum_u64(B.bucket_unique->as<uint64_t>(), c->dense_off.as<uint64_t>(), nbuckets,
                               c->dense_off.as<uint64_t>() + nbuckets, c->ws, s));
     FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
     c->distinct_pending = true;
-    if (!c->want_dense) {
-        // the result stays bucket-major (no compaction pass): the buckets' outputs are the result
-        HIP_TRY(launch_bin_offsets(B.flag_scan->as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
-                                   c->bin_off.as<uint64_t>(), s));
-        c->gapped = true;
-        c->dense_ready = false;
-        c->res_keys = okb.as<uint64_t>();
-        c->res_nbuckets = nbuckets;
-        c->res_F = F;
-        c->res_fs = B.flag_scan->as<uint64_t>();
-        return FK_OK;
-    }
-    c->gapped = false;
-    // the dense result sized for every key (a bound on the distinct keys) when that is at most a
-    // tenth of the device and fits twice over in its free memory: the compaction is then queued without waiting for the distinct total,
-    // which arrives with the bin offsets (resolve_distinct); else the total is read first
-    const uint64_t bound_keys = total_kmers * 8 * c->KW, bound_counts = total_kmers * 4;
-    bool bounded = c->dense_keys.bytes >= bound_keys && c->dense_counts.bytes >= bound_counts;
-    if (!bounded) {
-        size_t free_b = 0, total_b = 0;
-        const uint64_t grow = bound_keys + bound_counts - std::min<uint64_t>(c->dense_keys.bytes + c->dense_counts.bytes,
-                                                                               bound_keys + bound_counts);
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (uint64_t)free_b > 2 * grow &&
-            grow <= (uint64_t)total_b / 10) {
-            FK_TRY(ensure(c->dense_keys, bound_keys));
-            FK_TRY(ensure(c->dense_counts, bound_counts));
-            bounded = true;
-        }
-        (void)hipGetLastError();
-    }
-    if (!bounded) {
-        uint64_t distinct = 0;
-        HIP_TRY(hipMemcpyAsync(&distinct, c->dense_off.as<uint64_t>() + nbuckets, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        htrace("sorted: distinct read");
-        FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
-        FK_TRY(ensure(c->dense_counts, distinct * 4));
-    }
-    HIP_TRY(launch_bucket_compact(c->KW, okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                  B.buckets->as<Bucket>(), nbuckets, c->dense_off.as<uint64_t>(),
-                                  c->dense_keys.as<uint64_t>(), c->dense_counts.as<uint32_t>(), s));
     HIP_TRY(launch_bin_offsets(B.flag_scan->as<uint64_t>(), c->dense_off.as<uint64_t>(), c->nlb, F, nbuckets,
                                c->bin_off.as<uint64_t>(), s));
+    c->gapped = true;
+    c->dense_ready = false;
+    c->res_keys = okb.as<uint64_t>();
+    c->res_nbuckets = nbuckets;
+    c->res_F = F;
+    c->res_fs = B.flag_scan->as<uint64_t>();
     return FK_OK;
 }
 
@@ -1874,7 +1713,7 @@ static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in
     uint64_t nb = 0;
     FK_TRY(sorted_count_buckets(c, pl, src_in, total_kmers, c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(),
                                 main_bufs(c), okb, &nb));
-    return sorted_result(c, pl.F, nb, total_kmers, okb, main_bufs(c));
+    return sorted_result(c, pl.F, nb, okb, main_bufs(c));
 }
 
 // After the bin offsets are on the host: the sorted count's distinct total is their last entry.
@@ -1900,7 +1739,9 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     hipStream_t s = c->stream;
     const uint32_t nlb = c->nlb, nchunks = (uint32_t)chunks.size();
     const uint32_t KW = (uint32_t)c->KW;
-    const double per_group = (KW == 1 ? 4096.0 : 2048.0) * c->lh_load;  // LH_TS / LH2_TS slots, half full
+    // LH_TS / LH2_TS slots, half full (0.35 / 0.25 of a table measured slower at configs[1] and the
+    // configs[2] shape, profiles/r04c_ht_load_ab.txt)
+    const double per_group = (KW == 1 ? 4096.0 : 2048.0) * 0.5;
     std::vector<uint8_t> flog(nlb, 0);
     std::vector<uint32_t> gbase(nlb + 1, 0);
     std::vector<uint64_t> rec_base(nlb + 1, 0), km_base(nlb + 1, 0);
@@ -1951,48 +1792,29 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     FK_TRY(ensure(c->lh_sp[0], (uint64_t)ngroups * 4 + 64));
     if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
     uint64_t *const pin = c->pin_ht.as<uint64_t>();
-    // 128-bit keys: the groups of more than lh_big_thr k-mers take larger tables instead of spilling
-    // most of their keys from the 2048-slot ones: up to lh_huge_thr k-mers 3072 slots (two 512-thread
-    // workgroups per CU), above it (or above lh_big_thr when lh_huge_thr is 0) 6144 slots (one
-    // 1024-thread workgroup per CU)
-    // 64-bit keys: groups whose expected distinct keys (k-mers x the last count's distinct ratio)
-    // pass ~3/4 of a 4096-slot table may take 8192 slots (FASTKMER_HT_BIG64: k-mers, -1 auto; default 0:
-    // off -- at k = 28 over a 3 Gbp genome every group overflows, and one 104 KB workgroup per CU
-    // measured 18.9 against 16.7 ms, profiles/r04c_ht5_big64.txt)
-    uint64_t nbig = 0, nmid = 0;
-    const uint32_t thr64 = c->lh_big64 >= 0 ? (uint32_t)c->lh_big64
-                                            : (uint32_t)std::min(4.0e9, 3072.0 / std::max(0.05, c->lh_ratio));
-    const uint32_t big_thr = KW == 2 ? c->lh_big_thr : thr64;
-    const uint32_t huge_thr = KW == 2 && big_thr && c->lh_huge_thr > big_thr ? c->lh_huge_thr : 0u;
+    // 128-bit keys: the groups of more than lh_big_thr k-mers take 6144-slot tables (one 1024-thread
+    // workgroup per CU) instead of spilling most of their keys from the 2048-slot ones.  (A 3072-slot
+    // tier between them and 8192-slot tables for 64-bit keys measured slower, profiles/r04c_ht4_mid_
+    // tier_probes.txt, r04c_ht5_big64.txt: at k = 28 over a 3 Gbp genome every group overflows.)
+    uint64_t nbig = 0;
+    const uint32_t big_thr = KW == 2 ? c->lh_big_thr : 0u;
     if (big_thr) {
-        FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 8 + 64));
-        uint32_t *const gl = c->lh_glist.as<uint32_t>();
-        HIP_TRY(launch_ht_big_list(groups, ngroups, huge_thr ? huge_thr : big_thr, 0u, gl, sp_total + 1, s));
-        if (huge_thr) HIP_TRY(launch_ht_big_list(groups, ngroups, big_thr, huge_thr, gl + ngroups, sp_total, s));
+        FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 4 + 64));
+        HIP_TRY(launch_ht_big_list(groups, ngroups, big_thr, 0u, c->lh_glist.as<uint32_t>(), sp_total + 1, s));
         HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
         HIP_TRY(hipStreamSynchronize(s));
         nbig = pin[1];
-        nmid = huge_thr ? pin[0] : 0;
     }
-    c->stats.ht_big_groups = nbig + nmid;
+    c->stats.ht_big_groups = nbig;
     HIP_TRY(launch_ht_combine(c->W, c->lh_recs.as<uint64_t>(), groups, nullptr, ngroups, c->cfg.k, 0,
                               c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
                               c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe, nullptr, nullptr,
-                              nbig + nmid ? big_thr : 0u));
-    if (nbig && KW == 2)
+                              nbig ? big_thr : 0u));
+    if (nbig)
         HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
                                          c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
                                          d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
-    else if (nbig)
-        HIP_TRY(launch_ht_combine64_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
-                                        c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
-                                        d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
-    if (nmid)
-        HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>() + ngroups,
-                                         (uint32_t)nmid, c->cfg.k, c->lh_spill[0].as<uint64_t>(),
-                                         c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
-                                         c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, true));
     // the groups that spilled, listed on the device (a parent each: its spill range and count)
     FK_TRY(ensure(c->lh_parents, (uint64_t)ngroups * sizeof(LhItem) + 64));
     HIP_TRY(launch_ht_spill_list(groups, c->lh_sp[0].as<uint32_t>(), ngroups, c->lh_parents.as<LhItem>(),
@@ -2019,7 +1841,7 @@ static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
         uint64_t *const pl = c->lh_plan.as<uint64_t>();
         uint64_t *const cnt = pl, *const nsub = pl + np, *const npad = pl + 2 * np, *const region = pl + 3 * np,
                        *const item_off = pl + 4 * np, *const pad_off = pl + 5 * np, *const tot = pl + 6 * np;
-        HIP_TRY(launch_ht_plan(par, (uint32_t)np, per_group, c->lh_subpart, cnt, nsub, npad, s));
+        HIP_TRY(launch_ht_plan(par, (uint32_t)np, per_group, 1, cnt, nsub, npad, s));
         HIP_TRY(scan_excl_sum_u64(cnt, region, np, tot, c->ws, s));
         HIP_TRY(scan_excl_sum_u64(nsub, item_off, np, tot + 1, c->ws, s));
         HIP_TRY(scan_excl_sum_u64(npad, pad_off, np, tot + 2, c->ws, s));
@@ -2150,7 +1972,7 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
         max_bin = std::max(max_bin, bkm[lb]);
     }
     HIP_TRY(hipEventRecord(c->ev[6], s));
-    if (c->cfg.use_ht && c->lh_mode && c->cfg.k <= 63)  // k = 64: no spare bit in the hi word (global tables)
+    if (c->cfg.use_ht && c->cfg.k <= 63)  // k = 64: no spare bit in the hi word (global tables)
         FK_TRY(reduce_ht_lds(c, chunks, bcb, bkm));
     else if (c->cfg.use_ht)
         FK_TRY(reduce_ht(c, nchunks, bkm));
@@ -2278,6 +2100,11 @@ FK_EXPORT int fk_set_grouped_emit(fk_ctx *c, int32_t enable) {
     c->grouped = enable != 0;
     c->mapped = false;
     if (!c->grouped) return FK_OK;
+    return build_group_table(c);
+}
+
+// The grouped emit's bin -> part table (part = destination * grp_nlb + the bin's local index there).
+static int build_group_table(fk_ctx *c) {
     std::vector<uint32_t> table((size_t)c->Bc);
     if (c->custom_owners) {
         // size-aware placement (fk_set_bin_owners, the same table on every rank): part = owner *
@@ -2354,166 +2181,23 @@ FK_EXPORT int fk_reduce_grouped(fk_ctx *c, const void *d_recv, uint64_t nrecv, c
 }
 
 // ---------------------------------------------------------------------------
-// per-piece counts and their merge (fk_merge.inc)
+// staged pieces: a job's input partitioned and expanded piece by piece while later pieces land
 // ---------------------------------------------------------------------------
 
 static void pieces_reset(fk_ctx *c) {
-    c->pre_done = false;
-    c->pre_np = 0;
-    c->npieces = 0;
     c->st_np = 0;
+    c->st_cut = 0;
     c->st_kmers = 0;
     c->pieces_void = false;
     c->tiles_counted = 0;
     c->segs_counted = 0;
-    c->acc_ms_part = c->acc_ms_count = c->acc_ms_merge = 0.0;
-}
-
-// Pieces are counted separately for the sorted count (its results merge in key order); the hash
-// count's table order does not, it counts the whole input at the end.
-// One rank counts pieces of its own input only without a communicator and with G == 1 (a context
-// of G > 1 ranks without one maps for a caller-driven exchange, fk_map_emit: its input holds
-// other ranks' records); with a communicator the received segments are the pieces.
-static bool piece_counting(const fk_ctx *c) {
-    return c->count_pieces && !c->pieces_void && !c->cfg.use_ht && (c->comm || c->G == 1);
-}
-
-static void swap_result(fk_ctx *c, fk_ctx::PieceRes &r) {
-    std::swap(r.keys, c->dense_keys);
-    std::swap(r.counts, c->dense_counts);
-    std::swap(r.bin_off, c->bin_off);
-    r.h_bin_off.swap(c->h_bin_off);
-    std::swap(r.distinct, c->distinct);
-}
-
-static void swap_res(fk_ctx::PieceRes &a, fk_ctx::PieceRes &b) {
-    std::swap(a.keys, b.keys);
-    std::swap(a.counts, b.counts);
-    std::swap(a.bin_off, b.bin_off);
-    a.h_bin_off.swap(b.h_bin_off);
-    std::swap(a.distinct, b.distinct);
-}
-
-static MergeSrc merge_src(const DevBuf &keys, const DevBuf &counts, const DevBuf &bin_off) {
-    MergeSrc m;
-    m.keys = keys.as<uint64_t>();
-    m.counts = counts.as<uint32_t>();
-    m.bin_off = bin_off.as<uint64_t>();
-    return m;
-}
-
-// out = the per-bin union of results a and b (fk_merge.inc).
-static int merge2(fk_ctx *c, const fk_ctx::PieceRes &a, const fk_ctx::PieceRes &b, DevBuf &okeys, DevBuf &ocounts,
-                  DevBuf &obin_off, std::vector<uint64_t> &oh_bin_off, uint64_t *odistinct) {
-    hipStream_t s = c->stream;
-    const uint32_t nlb = c->nlb;
-    const double t0 = now_ms();
-    // every bin's first tile (bins have ceil(n / MERGE_TILE) >= 1 tiles), staged in pinned memory
-    htrace("merge2: enter");
-    if (c->pin_merge.ensure(((size_t)nlb + 1) * 4)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-    uint32_t *bin_tile0 = c->pin_merge.as<uint32_t>();
-    uint64_t ntiles = 0;
-    for (uint32_t lb = 0; lb < nlb; ++lb) {
-        const uint64_t n = a.h_bin_off[lb + 1] - a.h_bin_off[lb] + b.h_bin_off[lb + 1] - b.h_bin_off[lb];
-        bin_tile0[lb] = (uint32_t)ntiles;
-        ntiles += std::max<uint64_t>(1, (n + MERGE_TILE - 1) / MERGE_TILE);
-    }
-    bin_tile0[nlb] = (uint32_t)ntiles;
-    if (!ntiles) {  // no local bins
-        oh_bin_off.assign(1, 0);
-        *odistinct = 0;
-        FK_TRY(ensure(obin_off, 8));
-        HIP_TRY(hipMemsetAsync(obin_off.p, 0, 8, s));
-        return FK_OK;
-    }
-    HIP_TRY(hipEventRecord(c->ev[6], s));
-    FK_TRY(ensure(c->m2_bin_tile0, ((uint64_t)nlb + 1) * 4));
-    FK_TRY(ensure(c->m2_split_a, (ntiles + 1) * 8));
-    FK_TRY(ensure(c->m2_split_b, (ntiles + 1) * 8));
-    FK_TRY(ensure(c->m2_bnd, (ntiles + 1) * 8));
-    FK_TRY(ensure(c->m2_tcount, ntiles * 4));
-    FK_TRY(ensure(c->m2_toff, (ntiles + 1) * 8));
-    FK_TRY(ensure(c->m2_keys, ntiles * MERGE_TILE * 8 * c->KW));
-    FK_TRY(ensure(c->m2_counts, ntiles * MERGE_TILE * 4));
-    HIP_TRY(hipMemcpyAsync(c->m2_bin_tile0.p, bin_tile0, ((uint64_t)nlb + 1) * 4, hipMemcpyHostToDevice, s));
-    htrace("merge2: launching");
-    HIP_TRY(launch_merge2(c->KW, merge_src(a.keys, a.counts, a.bin_off), merge_src(b.keys, b.counts, b.bin_off),
-                          c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles,
-                          c->m2_split_a.as<uint64_t>(), c->m2_split_b.as<uint64_t>(), c->m2_bnd.as<uint64_t>(),
-                          c->m2_tcount.as<uint32_t>(), c->m2_keys.as<uint64_t>(), c->m2_counts.as<uint32_t>(), s));
-    HIP_TRY(scan_excl_sum_u32_to_u64(c->m2_tcount.as<uint32_t>(), c->m2_toff.as<uint64_t>(), ntiles,
-                                     c->m2_toff.as<uint64_t>() + ntiles, c->ws, s));
-    uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, c->m2_toff.as<uint64_t>() + ntiles, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    htrace("merge2: total read");
-    FK_TRY(ensure(okeys, total * 8 * c->KW));
-    FK_TRY(ensure(ocounts, total * 4));
-    FK_TRY(ensure(obin_off, ((uint64_t)nlb + 1) * 8));
-    HIP_TRY(launch_merge2_pack(c->KW, c->m2_tcount.as<uint32_t>(), c->m2_toff.as<uint64_t>(),
-                               c->m2_bin_tile0.as<uint32_t>(), nlb, ntiles, c->m2_keys.as<uint64_t>(),
-                               c->m2_counts.as<uint32_t>(), okeys.as<uint64_t>(), ocounts.as<uint32_t>(),
-                               obin_off.as<uint64_t>(), s));
-    HIP_TRY(hipEventRecord(c->ev[7], s));
-    oh_bin_off.assign((size_t)nlb + 1, 0);
-    if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-    HIP_TRY(hipMemcpyAsync(c->pin_down.p, obin_off.p, ((uint64_t)nlb + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    memcpy(oh_bin_off.data(), c->pin_down.p, ((size_t)nlb + 1) * 8);
-    *odistinct = oh_bin_off[nlb];
-    htrace("merge2: bin offsets read");
-    c->acc_ms_merge += ev_ms(c->ev[6], c->ev[7]);
-    c->stats.ms_total += now_ms() - t0;
-    return FK_OK;
-}
-
-// Counts one piece (`count` writes the context's result buffers; the piece slot's buffers stand
-// in for them meanwhile) and merges it into the running result.  With `last`, the merge goes to
-// the context's result buffers: the job's result.
-template <class F>
-static int count_piece(fk_ctx *c, F count, bool last) {
-    htrace("count_piece: enter");
-    swap_result(c, c->tmp);
-    c->want_dense = true;  // piece results are merged (fk_merge.inc reads dense arrays)
-    const int rc = count();
-    c->want_dense = false;
-    c->gapped = false;
-    swap_result(c, c->tmp);
-    if (rc) return rc;
-    c->acc_ms_part += c->stats.ms_partition;
-    c->acc_ms_count += c->stats.ms_count;
-    c->have_result = false;
-    if (c->npieces == 0) {
-        if (last) swap_result(c, c->tmp);
-        else swap_res(c->acc, c->tmp);
-    } else if (!last) {
-        FK_TRY(merge2(c, c->acc, c->tmp, c->acc2.keys, c->acc2.counts, c->acc2.bin_off, c->acc2.h_bin_off,
-                      &c->acc2.distinct));
-        swap_res(c->acc, c->acc2);
-    } else {
-        FK_TRY(merge2(c, c->acc, c->tmp, c->dense_keys, c->dense_counts, c->bin_off, c->h_bin_off, &c->distinct));
-    }
-    c->npieces += 1;
-    return FK_OK;
-}
-
-// The job's result from the counted pieces: the last merge wrote it, or one piece is all there is.
-static void finish_pieces(fk_ctx *c, bool merged_last) {
-    if (!merged_last) swap_result(c, c->acc);
-    c->stats.ms_partition = c->acc_ms_part;
-    c->stats.ms_count = c->acc_ms_count;
-    c->stats.ms_merge = c->acc_ms_merge;
-    c->stats.pieces_counted = c->npieces;
-    c->stats.distinct = c->distinct;
-    c->have_result = true;
 }
 
 // ---- staged pieces (sorted count, k <= 32): one rank's landed pieces, or the received segments
+// (the hash count and k = 64 count the whole input after the last byte; so do the test hook that
+// routes every bucket through the streaming path and the bucket-kernel probes)
 static bool staged_ok(const fk_ctx *c) {
-    const bool tier_ok = c->KW == 1 ? wave_staged_supported(c->wave_cap, c->wave_slots, c->wave_bpw)
-                                    : c->cfg.k <= 63 && wave128_staged_supported(c->wave_slots);
-    return c->piece_mode == 1 && tier_ok && !c->cfg.use_ht && c->count_mode == 1 && c->dbg_phase == 99 &&
-           !c->force_large && c->expand_levels >= 2;
+    return !c->cfg.use_ht && c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
 }
 static bool staged_eligible(const fk_ctx *c) { return staged_ok(c) && c->G == 1 && !c->comm; }
 
@@ -2540,7 +2224,6 @@ static int staged_expand_chunks(fk_ctx *c, uint32_t nchunks, const std::vector<u
     // scattered to its cells in one pass.  Off since level 2 sizes its workgroups to the keys per
     // super-cell (a 15 % piece: 1.14 ms one-pass against ~0.75 ms for both levels).
     SortedPlan pl = c->st_plan;
-    if (frac > 0.0 && frac < c->st_one_level && pl.F <= MAX_FINE_BITS - 1) pl.two_level = false;
     HIP_TRY(hipEventRecord(c->st_ev[4 * p + 2], s));
     FK_TRY(sorted_expand(c, pl, nchunks, pk, c->st_keys[p], c->st_cb[p]));
     const uint64_t ncell_all = (uint64_t)c->nlb << c->st_plan.F;
@@ -2565,120 +2248,6 @@ static int staged_expand(fk_ctx *c, const RecSrc &src, double frac) {
     return staged_expand_chunks(c, (uint32_t)chunks.size(), bkm, frac);
 }
 
-// Pre-count (one rank, k <= 32): worth it when the input is redundant -- the final count then
-// merges the pre-counted distinct keys (far fewer than the k-mers they stand for) with the last
-// pieces' k-mers.  Without redundancy the pre-counted entries are nearly as many as the k-mers and
-// the pre-count is extra work.
-static bool precount_ok(const fk_ctx *c) {
-    if (c->precount == 0 || c->KW != 1 || !staged_eligible(c)) return false;
-    return c->precount == 1 || (c->job_ratio >= 0.0 && c->job_ratio < 0.4);
-}
-
-// The buckets of the pieces expanded so far, counted while later pieces land: a bucket cut over
-// their summed cell totals (pre_total), each bucket's distinct keys ascending with counts at its
-// first slot of pre_keys / pre_counts (bucket-major), pre_unique per bucket.
-static int staged_precount(fk_ctx *c) {
-    hipStream_t s = c->stream;
-    const SortedPlan pl = c->st_plan;
-    const uint64_t ncell_all = (uint64_t)c->nlb << pl.F;
-    HIP_TRY(hipEventRecord(c->pre_ev[0], s));
-    FK_TRY(ensure(c->pre_total, ncell_all * 8));
-    FK_TRY(ensure(c->pre_base, (ncell_all + 1) * 8));
-    HIP_TRY(hipMemcpyAsync(c->pre_total.p, c->st_total.p, ncell_all * 8, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(scan_excl_sum_u64(c->pre_total.as<uint64_t>(), c->pre_base.as<uint64_t>(), ncell_all,
-                              c->pre_base.as<uint64_t>() + ncell_all, c->ws, s));
-    BucketSrc src{nullptr, pl.F};
-    src.np = (int)c->st_np;
-    for (uint32_t p = 0; p < c->st_np; ++p) {
-        src.pk[p] = c->st_keys[p].as<uint64_t>();
-        src.pcb[p] = c->st_cb[p].as<uint64_t>();
-    }
-    CountBufs B{&c->pre_flags, &c->pre_flag_scan, &c->pre_buckets, &c->pre_unique, &c->pre_tier_list,
-                &c->pre_piece_starts, &c->pre_counts};
-    uint64_t nb = 0;
-    FK_TRY(sorted_count_buckets(c, pl, src, c->st_kmers, c->pre_total.as<uint64_t>(), c->pre_base.as<uint64_t>(), B,
-                                c->pre_keys, &nb));
-    HIP_TRY(hipEventRecord(c->pre_ev[1], s));
-    c->pre_nb = nb;
-    c->pre_np = c->st_np;
-    c->pre_kmers = c->st_kmers;
-    c->pre_done = true;
-    htrace("staged: pre-count queued");
-    return FK_OK;
-}
-
-// The final count of a pre-counted job: the pre-count's bucket cut over the job's cells (B2); a
-// bucket whose pre-counted entries plus the later pieces' keys fit a wave is counted from them
-// (k_bucket_merge64_wave), the others from every piece's raw keys by the usual tiers.
-static int staged_count_merge(fk_ctx *c, const SortedPlan &pl) {
-    hipStream_t s = c->stream;
-    const int k = c->cfg.k;
-    const uint64_t nb = c->pre_nb, total = c->st_kmers;
-    FK_TRY(ensure(c->buckets, nb * sizeof(Bucket) + 16));
-    FK_TRY(ensure(c->out_keys, total * 8));
-    FK_TRY(ensure(c->out_counts, total * 4));
-    FK_TRY(ensure(c->bucket_unique, (nb + 1) * 8));
-    FK_TRY(ensure(c->tier_list, nb * 16 + 16));
-    FK_TRY(ensure(c->misc, 64));
-    HIP_TRY(launch_bucket_write(c->cell_base.as<uint64_t>(), c->pre_flags.as<uint32_t>(), c->pre_flag_scan.as<uint64_t>(),
-                                c->nlb, pl.F, nb, total, c->buckets.as<Bucket>(), s));
-    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
-    uint32_t *lists = c->tier_list.as<uint32_t>();
-    HIP_TRY(launch_bucket_tiers_merge(c->pre_buckets.as<Bucket>(), c->pre_unique.as<uint64_t>(), c->buckets.as<Bucket>(),
-                                      nb, pl.wave_cap, pl.cap, c->bucket_unique.as<uint64_t>(), lists,
-                                      c->misc.as<unsigned int>(), s));
-    if (c->pin_tier.ensure(16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-    HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 16, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    uint32_t nt[4];
-    memcpy(nt, c->pin_tier.p, 16);
-    htrace("staged: merge tiers read");
-    BucketSrc last{nullptr, pl.F}, all{nullptr, pl.F};
-    last.np = (int)(c->st_np - c->pre_np);
-    all.np = (int)c->st_np;
-    for (uint32_t p = 0; p < c->st_np; ++p) {
-        all.pk[p] = c->st_keys[p].as<uint64_t>();
-        all.pcb[p] = c->st_cb[p].as<uint64_t>();
-        if (p >= c->pre_np) {
-            last.pk[p - c->pre_np] = all.pk[p];
-            last.pcb[p - c->pre_np] = all.pcb[p];
-        }
-    }
-    uint64_t *ok = c->out_keys.as<uint64_t>(), *bu = c->bucket_unique.as<uint64_t>();
-    uint32_t *oc = c->out_counts.as<uint32_t>();
-    const Bucket *b2 = c->buckets.as<Bucket>();
-    if (nt[0]) {
-        if (last.np < 1) return set_err(FK_E_STATE, "pre-counted buckets without later pieces");
-        HIP_TRY(launch_bucket_merge64_wave(c->pre_keys.as<uint64_t>(), c->pre_counts.as<uint32_t>(),
-                                           c->pre_buckets.as<Bucket>(), c->pre_unique.as<uint64_t>(), last, b2, lists,
-                                           nt[0], k, ok, oc, bu, s));
-    }
-    if (nt[1])
-        HIP_TRY(launch_bucket_count64_wave(all, b2, nt[1], k, ok, oc, bu, c->wave_bpw, c->wave_cap, c->wave_slots,
-                                           lists + nb, s));
-    if (nt[2])
-        HIP_TRY(launch_bucket_count64(all, b2, nt[2], k, ok, oc, bu, c->misc.as<unsigned long long>() + 3, pl.cap, 99,
-                                      lists + 2 * nb, s));
-    uint64_t nlarge = 0;
-    if (nt[3]) {
-        HIP_TRY(launch_bucket_count64_big(all, b2, nt[3], k, ok, oc, bu, c->misc.as<unsigned long long>() + 2,
-                                          lists + 3 * nb, s));
-        HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (nlarge) {
-            FK_TRY(ensure(c->scratch, total * 8));
-            HIP_TRY(launch_bucket_sort_large(1, all, b2, nt[3], k, c->scratch.as<uint64_t>(), ok, oc, bu,
-                                             lists + 3 * nb, s));
-        }
-    }
-    c->stats.buckets = nb;
-    c->stats.fine_bits = (uint64_t)pl.F;
-    c->stats.oversize_buckets = nlarge;
-    CountBufs B{&c->pre_flags, &c->pre_flag_scan, &c->buckets, &c->bucket_unique, &c->tier_list, &c->piece_starts,
-                &c->out_counts};
-    return sorted_result(c, pl.F, nb, total, c->out_keys, B);
-}
-
 // The job's count over the staged pieces: buckets over the summed cell totals, each bucket's keys
 // read from every piece (BucketSrc pieces), the dense result and its bin offsets.
 static int staged_count(fk_ctx *c) {
@@ -2692,17 +2261,13 @@ static int staged_count(fk_ctx *c) {
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
                               c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
-    if (c->pre_done && c->st_np > c->pre_np) {
-        FK_TRY(staged_count_merge(c, pl));
-    } else {
-        BucketSrc src{nullptr, pl.F};
-        src.np = (int)c->st_np;
-        for (uint32_t p = 0; p < c->st_np; ++p) {
-            src.pk[p] = c->st_keys[p].as<uint64_t>();
-            src.pcb[p] = c->st_cb[p].as<uint64_t>();
-        }
-        FK_TRY(sorted_count(c, pl, src, c->st_kmers));
+    BucketSrc src{nullptr, pl.F};
+    src.np = (int)c->st_np;
+    for (uint32_t p = 0; p < c->st_np; ++p) {
+        src.pk[p] = c->st_keys[p].as<uint64_t>();
+        src.pcb[p] = c->st_cb[p].as<uint64_t>();
     }
+    FK_TRY(sorted_count(c, pl, src, c->st_kmers));
     HIP_TRY(hipEventRecord(c->ev[7], s));
     c->h_bin_off.assign((size_t)nlb + 1, 0);
     if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
@@ -2717,8 +2282,8 @@ static int staged_count(fk_ctx *c) {
         mx += ev_ms(c->st_ev[4 * p + 2], c->st_ev[4 * p + 3]);
     }
     c->stats.ms_partition = mp;
-    c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]) + (c->pre_done ? ev_ms(c->pre_ev[0], c->pre_ev[1]) : 0.0);
-    c->stats.precounted = c->pre_done ? 1u : 0u;
+    c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]);
+    c->stats.precounted = 0;
     c->stats.ms_merge = 0.0;
     c->stats.pieces_counted = c->st_np;
     c->stats.records_received = c->nrec;
@@ -2728,37 +2293,26 @@ static int staged_count(fk_ctx *c) {
     return FK_OK;
 }
 
-// One rank: counts the tiles mapped since the last piece once they cover a piece (fk_ingest).
+// One rank: stages the tiles mapped since the last piece once they cover a piece (fk_ingest).
 // The fused map's fallback flag is read first: a flagged input is counted whole by fk_finish.
-// Piece ends: with the job's size known (one fk_ingest call) and no FASTKMER_PIECE_BYTES, at the
-// fractions piece_cuts of it (default one cut at 55 %: the first piece's count runs while the rest
-// lands, and the last piece -- counted and merged after the last byte lands -- is the smaller one);
-// jobs under 2 * MIN_PIECE are counted whole.  A streamed job: every piece_bytes.
+// Piece ends: with the job's size known (one fk_ingest call, or fk_ingest_reserve) and no
+// FASTKMER_PIECE_BYTES, at the fractions st_cuts of it (the last piece -- expanded after the last byte
+// lands -- is the smallest); jobs under 2 * MIN_PIECE are counted whole.  A streamed job of unknown
+// size: every piece_bytes.  At most STAGE_MAXP - 1 pieces before fk_finish stages the last one.
 static bool local_piece_due(const fk_ctx *c) {
     constexpr uint64_t MIN_PIECE = 256ull << 20;
-    // Pieces pay when the input is redundant: every piece holds most of the distinct k-mers, so the
-    // work that scales with distinct k-mers (the rank and output of the count, the compaction, the
-    // merge) is paid once per piece.  Past half distinct (the last job's ratio) one count after the
-    // last byte is the shorter path (configs[3] shape, 93 % distinct: 48.2 ms per GB with a piece,
-    // ~42.7 without).
-    // Staged pieces (expanded only, counted once at the end) repeat no work: they always pay, and
-    // the last one -- expanded after the last byte lands -- is the smallest.
-    const bool staged = staged_eligible(c);
-    if (staged && c->st_np >= (uint32_t)STAGE_MAXP - 1) return false;
-    if (!staged && c->job_ratio > 0.5 && !c->piece_bytes_set) return false;
-    const std::vector<double> &cuts = staged ? c->st_cuts : c->piece_cuts;
-    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    if (c->st_np >= (uint32_t)STAGE_MAXP - 1) return false;
+    const uint64_t tile = fm_tile_bytes(FUSED_NT);
     if (c->job_bytes && !c->piece_bytes_set) {
-        if (c->job_bytes < 2 * MIN_PIECE || c->npieces >= cuts.size()) return false;
-        const uint64_t end = (uint64_t)(cuts[c->npieces] * (double)c->job_bytes);
+        if (c->job_bytes < 2 * MIN_PIECE || c->st_cut >= c->st_cuts.size()) return false;
+        const uint64_t end = (uint64_t)(c->st_cuts[c->st_cut] * (double)c->job_bytes);
         return c->pm_tiles * tile >= end && (c->pm_tiles - c->tiles_counted) * tile >= MIN_PIECE / 2;
     }
     return (c->pm_tiles - c->tiles_counted) * tile >= c->piece_bytes;
 }
 
 static int local_maybe_piece(fk_ctx *c) {
-    if (!piece_counting(c)) return FK_OK;
-    if (!local_piece_due(c)) return FK_OK;
+    if (!staged_eligible(c) || c->pieces_void || !local_piece_due(c)) return FK_OK;
     uint64_t h[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2769,15 +2323,8 @@ static int local_maybe_piece(fk_ctx *c) {
     const uint64_t t0 = c->tiles_counted, nt = c->pm_tiles - t0;
     const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
     c->tiles_counted = c->pm_tiles;
-    if (staged_eligible(c)) {
-        const uint32_t np0 = c->st_np;
-        FK_TRY(staged_expand(c, src, c->job_bytes ? (double)(nt * fm_tile_bytes(c->fused_nt)) / (double)c->job_bytes
-                                                  : 0.0));
-        if (c->st_np > np0) c->npieces += 1;  // (a piece without k-mers adds none)
-        if (!c->pre_done && c->st_np == c->pre_at && precount_ok(c)) FK_TRY(staged_precount(c));
-        return FK_OK;
-    }
-    return count_piece(c, [&] { return reduce_src(c, src); }, false);
+    c->st_cut += 1;
+    return staged_expand(c, src, c->job_bytes ? (double)(nt * fm_tile_bytes(FUSED_NT)) / (double)c->job_bytes : 0.0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2901,7 +2448,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
         // once the first pieces show the records per FASTA byte)
         uint64_t want = c->xch.recv_used + recv_rec;
         if (c->xch.expect_bytes && c->xch.tiles_sent) {
-            const double covered = (double)c->xch.tiles_sent * (double)fm_tile_bytes(c->fused_nt);
+            const double covered = (double)c->xch.tiles_sent * (double)fm_tile_bytes(FUSED_NT);
             want = std::max<uint64_t>(want, (uint64_t)((double)want * (double)c->xch.expect_bytes / covered * 1.1));
         }
         HIP_TRY(hipStreamSynchronize(cs));
@@ -2970,21 +2517,6 @@ static int segment_ranges(fk_ctx *c, size_t s0, size_t s1, std::vector<std::vect
     return FK_OK;
 }
 
-// Counts the received segments [segs_counted, s1) as one piece result, once the comm stream has
-// delivered them (the end event of the step of the last one).
-static int xch_count_segments(fk_ctx *c, size_t s1, bool last) {
-    if (s1 <= c->segs_counted) return FK_OK;
-    const uint64_t step = c->xch.segs[s1 - 1].step;
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->xev[2 * step + 1], 0));
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges;
-    std::vector<uint64_t> bkm;
-    uint64_t nrecv = 0;
-    FK_TRY(segment_ranges(c, c->segs_counted, s1, ranges, bkm, &nrecv));
-    c->segs_counted = s1;
-    return count_piece(c, [&] { return reduce_ranges(c, c->xrecv.as<uint64_t>(), nrecv, ranges, bkm, now_ms()); },
-                       last);
-}
-
 // With a communicator and staged pieces: expands the received segments [segs_counted, s1) as one
 // staged piece (they arrive grouped by local bin: no partition), once the comm stream has
 // delivered them.  `frac` = their estimated fraction of what this rank receives in the job.
@@ -3016,7 +2548,7 @@ static int xch_stage_segments(fk_ctx *c, size_t s1, double frac) {
 // sent so far; 0 when the input's size is unknown).
 static double xch_recv_frac(const fk_ctx *c, uint64_t recs) {
     if (!c->xch.expect_bytes || !c->xch.tiles_sent || !c->xch.recv_used) return 0.0;
-    const double sent = (double)c->xch.tiles_sent * (double)fm_tile_bytes(c->fused_nt);
+    const double sent = (double)c->xch.tiles_sent * (double)fm_tile_bytes(FUSED_NT);
     const double est = (double)c->xch.recv_used * (double)c->xch.expect_bytes / sent;
     return est > 0.0 ? std::min(1.0, (double)recs / est) : 0.0;
 }
@@ -3033,16 +2565,11 @@ static int xch_maybe_stage(fk_ctx *c, size_t s1) {
     // path's pieces): the last piece -- expanded after the last byte -- is the smallest.  (Staging at
     // every quarter left ~30 % of a 6.25 GB rank for fk_finish: 61.7 ms after it against 47.7 for
     // the local path, profiles/r04c_xch_tail.txt.)
-    if (frac > 0.0 && !c->xch_cuts) {
-        if (frac < 1.0 / STAGE_MAXP) return FK_OK;
-    } else if (frac > 0.0) {
+    if (frac > 0.0) {
         if (c->st_np >= (uint32_t)c->st_cuts.size()) return FK_OK;
         if (xch_recv_frac(c, before + recs) < c->st_cuts[c->st_np]) return FK_OK;
     }
-    const uint32_t np0 = c->st_np;
-    FK_TRY(xch_stage_segments(c, s1, frac));
-    if (c->st_np > np0) c->npieces += 1;  // (segments without k-mers add no piece)
-    return FK_OK;
+    return xch_stage_segments(c, s1, frac);
 }
 
 // fk_ingest: sends the tiles mapped since the last piece once they cover a piece.  The fused
@@ -3050,7 +2577,7 @@ static int xch_maybe_stage(fk_ctx *c, size_t s1) {
 // whole, retracting the pieces sent so far.
 static int xch_maybe_piece(fk_ctx *c) {
     if (c->xch.stop_pieces || c->xch.sent_final) return FK_OK;
-    const uint64_t tile = fm_tile_bytes(c->fused_nt);
+    const uint64_t tile = fm_tile_bytes(FUSED_NT);
     if ((c->pm_tiles - c->xch.tiles_sent) * tile < c->piece_bytes) return FK_OK;
     uint64_t h[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
@@ -3066,10 +2593,7 @@ static int xch_maybe_piece(fk_ctx *c) {
     const int rc = xch_step(c, &src, 0);
     if (rc) return comm_fail(c, rc);
     // the records of the earlier steps are counted (staged: expanded) while this step's are on the wire
-    if (piece_counting(c) && before > c->segs_counted) {
-        if (staged_ok(c)) FK_TRY(xch_maybe_stage(c, before));
-        else FK_TRY(xch_count_segments(c, before, false));
-    }
+    if (staged_ok(c) && !c->pieces_void && before > c->segs_counted) FK_TRY(xch_maybe_stage(c, before));
     return FK_OK;
 }
 
@@ -3109,11 +2633,6 @@ static int finish_exchange(fk_ctx *c) {
             FK_TRY(xch_stage_segments(c, c->xch.segs.size(), nrecv ? (double)recs / (double)nrecv : 0.0));
         }
         FK_TRY(staged_count(c));
-    } else if (c->npieces && !c->pieces_void) {
-        // earlier steps were counted while later ones were on the wire: the rest, merged in
-        const bool more = c->segs_counted < c->xch.segs.size();
-        if (more) FK_TRY(xch_count_segments(c, c->xch.segs.size(), true));
-        finish_pieces(c, more);
     } else {
         std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges;
         std::vector<uint64_t> bkm;
@@ -3152,31 +2671,14 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
         if (c->rec_tiles > c->tiles_counted) {
             const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
             FK_TRY(staged_expand(c, fused_src(c, t0, nt, nt * map_fused_tcap()),
-                                 c->job_bytes ? (double)(nt * fm_tile_bytes(c->fused_nt)) / (double)c->job_bytes : 0.0));
+                                 c->job_bytes ? (double)(nt * fm_tile_bytes(FUSED_NT)) / (double)c->job_bytes : 0.0));
         }
         FK_TRY(staged_count(c));
         pieces_reset(c);
-        if (c->nkmers) c->job_ratio = (double)c->distinct / (double)c->nkmers;
-        return FK_OK;
-    }
-    if (c->npieces && c->rec_tiled && !c->pieces_void && c->tiles_counted <= c->rec_tiles) {
-        // pieces were counted while the input landed: the last piece, merged in
-        const bool more = c->rec_tiles > c->tiles_counted;
-        if (more) {
-            const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
-            const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
-            FK_TRY(count_piece(c, [&] { return reduce_src(c, src); }, true));
-        }
-        finish_pieces(c, more);
-        c->stats.records_received = c->nrec;
-        pieces_reset(c);
-        if (c->nkmers) c->job_ratio = (double)c->distinct / (double)c->nkmers;
         return FK_OK;
     }
     pieces_reset(c);
-    FK_TRY(reduce_src(c, map_src(c)));
-    if (c->nkmers) c->job_ratio = (double)c->distinct / (double)c->nkmers;
-    return FK_OK;
+    return reduce_src(c, map_src(c));
 }
 
 static int attach_comm(fk_ctx *c, fk::Comm *comm) {
@@ -3335,9 +2837,18 @@ static int split_sample(const char *path, int32_t world, int32_t rank, int32_t k
             }
             out.insert(out.end(), buf.begin() + a, buf.begin() + e);
         } else {  // a block of the sequence as one record
+            // the block's first line is dropped (it may be the tail of a header line: the block
+            // started inside it, or the file's first header), and the block ends at the next
+            // header line (a later record's name is not sequence)
+            size_t a = 0;
+            while (a < buf.size() && buf[a] != '\n') ++a;
+            a = a < buf.size() ? a + 1 : buf.size();
+            size_t e = a;
+            while (e < buf.size() && !(buf[e] == '>' && buf[e - 1] == '\n')) ++e;
+            if (e <= a) continue;
             const uint8_t h[3] = {'\n', '>', '\n'};
             out.insert(out.end(), h, h + 3);
-            out.insert(out.end(), buf.begin(), buf.end());
+            out.insert(out.end(), buf.begin() + a, buf.begin() + e);
         }
     }
     if (seq == 1) out.push_back('\n');
@@ -3348,7 +2859,8 @@ static int split_sample(const char *path, int32_t world, int32_t rank, int32_t k
 FK_EXPORT int fk_balance_bins_file(fk_ctx *c, const char *path, int32_t world, int32_t rank, double fraction) {
     if (!c || !path) return set_err(FK_E_INVALID, "null argument");
     std::vector<uint8_t> sample;
-    int rc = split_sample(path, world, rank, c->cfg.k, c->cfg.sequence_type, fraction, sample);
+    int rc = check_split_rank(c, world, rank, "fk_balance_bins_file");
+    if (!rc) rc = split_sample(path, world, rank, c->cfg.k, c->cfg.sequence_type, fraction, sample);
     if (!rc) rc = balance_from_sample(c, sample.data(), sample.size());
     return rc && c->comm ? comm_fail(c, rc) : rc;
 }
@@ -3467,9 +2979,7 @@ FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t
     const int KW = k <= 32 ? 1 : 2;
     const uint32_t cap = KW == 1 ? WAVE_BUCKET_CAP : WAVE128_BUCKET_CAP;
     if (n == 0 || n > cap) return set_err(FK_E_RANGE, "a wave bucket holds 1..%u keys", cap);
-    const bool small = KW == 1 ? slots == 768 : slots == 384;
-    if (!(KW == 1 ? (slots == 768 || slots == 1024) : (slots == 384 || slots == 512)))
-        return set_err(FK_E_INVALID, "slots: 768 / 1024 (k <= 32), 384 / 512 (k > 32)");
+    if (slots != (KW == 1 ? 768 : 384)) return set_err(FK_E_INVALID, "slots: 768 (k <= 32) or 384 (k > 32)");
     const int sh = 2 * k - F;
     for (uint32_t i = 0; i < n; ++i) {  // every key inside the bucket's cells
         const uint64_t hi = KW == 1 ? 0 : keys[2 * i], lo = KW == 1 ? keys[i] : keys[2 * i + 1];
@@ -3490,10 +3000,9 @@ FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t
     if (e == hipSuccess) e = hipMemcpy(db.p, &b, sizeof(Bucket), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = KW == 1 ? launch_bucket_count64_wave(BucketSrc{dk.as<uint64_t>(), F}, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
-                                                 doc.as<uint32_t>(), du.as<uint64_t>(), 1, WAVE_BUCKET_CAP,
-                                                 (uint32_t)slots, nullptr, nullptr)
+                                                 doc.as<uint32_t>(), du.as<uint64_t>(), nullptr, nullptr)
                     : launch_bucket_count128_wave(BucketSrc{dk.as<uint64_t>(), F}, db.as<Bucket>(), 1, k, dok.as<uint64_t>(),
-                                                  doc.as<uint32_t>(), du.as<uint64_t>(), small, nullptr);
+                                                  doc.as<uint32_t>(), du.as<uint64_t>(), nullptr);
     uint64_t U = 0;
     if (e == hipSuccess) e = hipMemcpy(&U, du.p, 8, hipMemcpyDeviceToHost);
     if (e == hipSuccess && U <= n) e = hipMemcpy(out_keys, dok.p, U * 8 * KW, hipMemcpyDeviceToHost);

@@ -194,17 +194,33 @@ class RcclComm : public Comm {
 // ---------------------------------------------------------------------------
 
 struct LocalGroup {
-    explicit LocalGroup(int n) : n(n) {
+    explicit LocalGroup(int n) : n(n), device(n, 0) {
         for (auto &v : slot) v.resize(n);
+        for (int p = 0; p < 2; ++p) ready[p].assign(n, nullptr), done[p].assign(n, nullptr);
+    }
+    // The ranks' events belong to the group, not to a rank: a peer may still wait on a rank's
+    // `done` event after that rank has left the job's last collective and been destroyed (its
+    // LocalComm gone), so they live until the last rank of the group is gone.
+    ~LocalGroup() {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        for (int r = 0; r < n; ++r) {
+            (void)hipSetDevice(device[r]);
+            for (int p = 0; p < 2; ++p) {
+                if (ready[p][r]) (void)hipEventDestroy(ready[p][r]);
+                if (done[p][r]) (void)hipEventDestroy(done[p][r]);
+            }
+        }
+        if (prev >= 0) (void)hipSetDevice(prev);
     }
     struct Slot {
         const uint64_t *in = nullptr;
         const uint8_t *send = nullptr;
         const uint64_t *soff = nullptr, *sbytes = nullptr;
-        hipEvent_t ready = nullptr, done = nullptr;
-        int device = 0;
     };
     int n;
+    std::vector<int> device;                       // rank -> HIP device
+    std::vector<hipEvent_t> ready[2], done[2];     // per collective parity, per rank
     std::mutex mu;
     std::condition_variable cv;
     uint64_t gen = 0;
@@ -249,21 +265,14 @@ class LocalComm : public Comm {
     }
     ~LocalComm() override {
         // a rank that leaves fails the group: peers blocked in (or entering) a collective return
-        // an error instead of waiting for it
+        // an error instead of waiting for it.  Its events stay with the group (see LocalGroup).
         g_->fail();
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        (void)hipSetDevice(dev_);
-        for (auto &e : ready_)
-            if (e) (void)hipEventDestroy(e);
-        for (auto &e : done_)
-            if (e) (void)hipEventDestroy(e);
-        if (prev >= 0) (void)hipSetDevice(prev);
     }
     int init(std::string &err) {
-        for (int i = 0; i < 2; ++i) {
-            COMM_HIP(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming));
-            COMM_HIP(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming));
+        g_->device[rank_] = dev_;
+        for (int p = 0; p < 2; ++p) {
+            COMM_HIP(hipEventCreateWithFlags(&g_->ready[p][rank_], hipEventDisableTiming));
+            COMM_HIP(hipEventCreateWithFlags(&g_->done[p][rank_], hipEventDisableTiming));
         }
         return 0;
     }
@@ -294,12 +303,11 @@ class LocalComm : public Comm {
                   const uint64_t *roff, const uint64_t *rbytes, hipStream_t s, std::string &err) override {
         const int p = next();
         auto &sl = g_->slot[p];
-        COMM_HIP(hipEventRecord(ready_[p], s));
+        hipEvent_t *ready = g_->ready[p].data(), *done = g_->done[p].data();
+        COMM_HIP(hipEventRecord(ready[rank_], s));
         sl[rank_].send = send;
         sl[rank_].soff = soff;
         sl[rank_].sbytes = sbytes;
-        sl[rank_].ready = ready_[p];
-        sl[rank_].device = dev_;
         if (g_->barrier(err)) return -1;
         int rc = 0;
         for (int r = 0; r < n_ && !rc; ++r) {
@@ -311,11 +319,11 @@ class LocalComm : public Comm {
                 break;
             }
             if (!nb) continue;
-            hipError_t e = hipStreamWaitEvent(s, sl[r].ready, 0);
+            hipError_t e = hipStreamWaitEvent(s, ready[r], 0);
             if (e == hipSuccess)
-                e = sl[r].device == dev_
+                e = g_->device[r] == dev_
                         ? hipMemcpyAsync(recv + roff[r], sl[r].send + sl[r].soff[rank_], nb, hipMemcpyDeviceToDevice, s)
-                        : hipMemcpyPeerAsync(recv + roff[r], dev_, sl[r].send + sl[r].soff[rank_], sl[r].device, nb,
+                        : hipMemcpyPeerAsync(recv + roff[r], dev_, sl[r].send + sl[r].soff[rank_], g_->device[r], nb,
                                              s);
             if (e != hipSuccess) {
                 err = hip_msg("in-process exchange copy", e);
@@ -326,12 +334,12 @@ class LocalComm : public Comm {
             g_->fail();
             return -1;
         }
-        COMM_HIP(hipEventRecord(done_[p], s));
-        sl[rank_].done = done_[p];
+        COMM_HIP(hipEventRecord(done[rank_], s));
         if (g_->barrier(err)) return -1;
-        // this rank's send buffer stays untouched until every peer has copied out of it
+        // this rank's send buffer stays untouched until every peer has copied out of it (the
+        // context's teardown synchronizes this stream before it frees the send buffer)
         for (int r = 0; r < n_; ++r)
-            if (r != rank_ && sbytes[r]) COMM_HIP(hipStreamWaitEvent(s, sl[r].done, 0));
+            if (r != rank_ && sbytes[r]) COMM_HIP(hipStreamWaitEvent(s, done[r], 0));
         return 0;
     }
 
@@ -342,7 +350,6 @@ class LocalComm : public Comm {
     std::shared_ptr<LocalGroup> g_;
     int dev_;
     uint64_t seq_ = 0;
-    hipEvent_t ready_[2] = {nullptr, nullptr}, done_[2] = {nullptr, nullptr};
 };
 
 }  // namespace

@@ -175,8 +175,9 @@ hipError_t launch_expand_hist(int W, const uint64_t *rec, const Chunk *chunks, u
                               uint32_t *hist, hipStream_t s);
 hipError_t launch_cell_prefix(const uint32_t *bin_chunk_begin, uint32_t nlbins, int F, uint32_t *hist,
                               uint64_t *cell_total, hipStream_t s);
+// one-level expansion (k = 64, W = 3 only)
 hipError_t launch_expand_scatter(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
-                                 const uint32_t *hist, const uint64_t *cell_base, uint64_t *keys, int wc, hipStream_t s);
+                                 const uint32_t *hist, const uint64_t *cell_base, uint64_t *keys, hipStream_t s);
 hipError_t launch_bucket_flags(const uint64_t *cell_base, const uint64_t *cell_total, uint32_t nlbins, int F,
                                uint32_t small_cap, uint32_t group, uint32_t *flags, hipStream_t s);
 hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags, const uint64_t *flag_scan,
@@ -193,13 +194,11 @@ constexpr uint32_t WAVE_BUCKET_CAP = 512;
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                                       bool small_tables, hipStream_t s);
+                                       hipStream_t s);
 hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
                                    uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
                                    const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s,
-                                   int l1_threads = 0, uint64_t nkeys = 0, int l2_threads = 0);
-hipError_t launch_expand_hist_sc(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k, int F,
-                                 int F2, uint64_t *cell_total, uint32_t *hist_sc, hipStream_t s);
+                                   int l1_threads = 0, uint64_t nkeys = 0);
 // pieces of bins (x = local bin, y / z = chunk range, w = whole bin): the same per piece, then the
 // earlier pieces' super-cell totals added (first_piece[i] = the bin's first piece)
 hipError_t launch_expand_hist_pieces(int KW, const uint64_t *rec, const Chunk *chunks, const uint4 *pieces,
@@ -214,23 +213,8 @@ hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbin
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
                                uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts, hipStream_t s);
 hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
-                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique, int bpw,
-                                      uint32_t wave_cap, uint32_t wave_slots, const uint32_t *list, hipStream_t s);
-// final count of a pre-counted staged job (k <= 32): tiers of the final buckets b2 (the cells of the
-// pre-count's buckets b1 over the whole job) and the wave kernel that counts a bucket from the
-// pre-counted entries (r1 at b1[q].begin, u1[q] of them, weights = their counts) plus the raw keys
-// of the later pieces (`last`, a staged-piece view)
-hipError_t launch_bucket_tiers_merge(const Bucket *b1, const uint64_t *u1, const Bucket *b2, uint64_t nb,
-                                     uint32_t wave_cap, uint32_t block_cap, uint64_t *bucket_unique, uint32_t *lists,
-                                     unsigned int *counts, hipStream_t s);
-hipError_t launch_bucket_merge64_wave(const uint64_t *r1_keys, const uint32_t *r1_counts, const Bucket *b1,
-                                      const uint64_t *u1, const BucketSrc &last, const Bucket *b2,
-                                      const uint32_t *list, uint64_t nlist, int k, uint64_t *out_keys,
-                                      uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s);
-// staged pieces (src.np > 0) in the wave tier: the default tier configuration only
-bool wave_staged_supported(uint32_t wave_cap, uint32_t wave_slots, int bpw);
-// staged pieces in the 128-bit wave tier: the default table size only
-bool wave128_staged_supported(uint32_t wave_slots);
+                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
+                                      const uint32_t *list, hipStream_t s);
 // dst[i] += src[i] (dst = src when `copy`)
 hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
 // skip_le: listed buckets of at most this many keys were counted by a wave tier (skipped)
@@ -315,39 +299,16 @@ hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, 
                              hipStream_t s, int probe = 0, const uint64_t *psrc = nullptr,
                              const uint32_t *sub_off = nullptr, uint32_t big_thr = 0);
 // 128-bit keys: round 1 of the groups of thr < k-mers <= hi (hi = 0: no bound; k_ht_big_list) in
-// 6144-slot tables, or (mid) 3072-slot ones
+// 6144-slot tables
 hipError_t launch_ht_big_list(const LhGroup *groups, uint32_t ngroups, uint32_t thr, uint32_t hi, uint32_t *glist,
                               unsigned long long *n_out, hipStream_t s);
-// 64-bit keys: round 1 of the listed heavy groups in 8192-slot tables
-hipError_t launch_ht_combine64_big(const uint64_t *src, const LhGroup *groups, const uint32_t *glist, uint32_t n,
-                                   int k, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
-                                   const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys,
-                                   uint32_t *ocnt, hipStream_t s);
 hipError_t launch_ht_combine128_big(const uint64_t *src, const LhGroup *groups, const uint32_t *glist, uint32_t n,
                                     int k, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
                                     const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys,
-                                    uint32_t *ocnt, hipStream_t s, bool mid = false);
+                                    uint32_t *ocnt, hipStream_t s);
 hipError_t launch_ht_gather(int KW, const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb,
                             const uint64_t *okeys, const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt,
                             hipStream_t s);
-
-// ---- merge of two count results (fk_merge.inc): the per-bin union, equal k-mers' counts added
-struct MergeSrc {          // one result
-    const uint64_t *keys;     // KW words per entry, ascending per bin
-    const uint32_t *counts;
-    const uint64_t *bin_off;  // [nlb + 1]
-};
-constexpr uint32_t MERGE_TILE = 1024;  // merged entries per workgroup (M2_TILE)
-// bin_tile0[nlb + 1]: every bin's first tile (a bin has ceil((na + nb) / MERGE_TILE) >= 1 tiles, in
-// bin order; bin_tile0[nlb] = ntiles); split_a / split_b / bnd: ntiles + 1 u64; tcount: ntiles;
-// sparse keys / counts: ntiles * MERGE_TILE entries (every tile's slot)
-hipError_t launch_merge2(int KW, const MergeSrc &A, const MergeSrc &B, const uint32_t *bin_tile0, uint32_t nlb,
-                         uint64_t ntiles, uint64_t *split_a, uint64_t *split_b, uint64_t *bnd, uint32_t *tcount,
-                         uint64_t *sparse_keys, uint32_t *sparse_counts, hipStream_t s);
-// toff = exclusive scan of tcount (ntiles + 1): the dense result and its bin offsets (nlb + 1)
-hipError_t launch_merge2_pack(int KW, const uint32_t *tcount, const uint64_t *toff, const uint32_t *bin_tile0,
-                              uint32_t nlb, uint64_t ntiles, const uint64_t *sparse_keys, const uint32_t *sparse_counts,
-                              uint64_t *out_keys, uint32_t *out_counts, uint64_t *bin_off, hipStream_t s);
 
 // ---- synthetic input
 hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);

@@ -344,5 +344,4 @@ hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWo
 #include "fk_synth.inc"
 #include "fk_format.inc"
 #include "fk_bin_signatures.inc"
-#include "fk_merge.inc"
 }  // namespace fk

@@ -83,13 +83,12 @@ typedef struct fk_stats {
     double ms_exchange;        /* sum over the steps of their record transfer time on the comm stream */
     double ms_exchange_tail;   /* fk_finish: the last piece posted -> every rank's records received */
     /* pieces counted while later ones were still being copied in / received (sorted count) */
-    uint64_t pieces_counted;   /* piece results merged by the last fk_finish (0: one count of the whole input) */
-    double ms_merge;           /* their k-way merge (k_merge_plan / k_merge_segments / k_merge_compact) */
-    uint64_t precounted;       /* 1: the job's first staged pieces were counted while the rest landed, the final
-                                  count merged them with the later pieces' k-mers */
+    uint64_t pieces_counted;   /* staged pieces of the last fk_finish (0: one count of the whole input) */
+    double ms_merge;           /* unused (0): staged pieces are counted once, never merged */
+    uint64_t precounted;       /* unused (0) */
     uint64_t block_buckets;    /* buckets above the wave tier of at most 2048 keys (mid wave tier, block kernel) */
     uint64_t big_buckets;      /* buckets above 2048 keys (the big-table kernel, then the large path) */
-    uint64_t ht_big_groups;    /* useHT, k > 32: groups counted in the 6144-slot tables (FASTKMER_HT_BIG) */
+    uint64_t ht_big_groups;    /* useHT, k > 32: groups counted in the 6144-slot tables */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
@@ -152,7 +151,8 @@ int fk_ingest_device(fk_ctx *ctx, const void *d_fasta, size_t n, int last);
  *     the next window is read while the last one is copied and mapped), the
  *     job's size announced first (fk_ingest_reserve).  Collective like
  *     fk_ingest with a communicator.  world / rank: the split (usually the
- *     context's n_ranks / rank). */
+ *     context's n_ranks / rank; with a communicator they must be, else
+ *     FK_E_INVALID). */
 int fk_split_bytes(const char *path, int32_t world, int32_t rank, int32_t k, int32_t sequence_type, uint8_t *out,
                    size_t cap, size_t *n);
 int fk_ingest_file_range(fk_ctx *ctx, const char *path, int32_t world, int32_t rank, uint64_t window_bytes);
@@ -200,7 +200,9 @@ int fk_finish(fk_ctx *ctx);
  *   fk_set_bin_owners: install owner[b] (the same table on every rank) before
  *     fk_map_emit / fk_reduce, or before a job's first fk_ingest with a
  *     communicator (the exchange then groups records by (owner, the bin's index
- *     among its owner's bins)); recomputes send_counts when already mapped. */
+ *     among its owner's bins)); when already mapped it recomputes send_counts
+ *     (and, with the grouped emit, fk_map_part_counts) under the new owners, so
+ *     fk_map_emit may follow directly. */
 int fk_map_bin_kmers(fk_ctx *ctx, uint64_t *kmers_per_bin);
 int fk_lpt_owners(const uint64_t *sizes, int32_t nbins, int32_t nranks, int32_t *owner);
 int fk_set_bin_owners(fk_ctx *ctx, const int32_t *owner, uint64_t *send_counts);
@@ -240,7 +242,8 @@ int fk_comm_allreduce_u64(fk_ctx *ctx, uint64_t *v, size_t n);
  * rank's own sample decides.
  *   fk_balance_bins: the caller's sample bytes (FASTA text);
  *   fk_balance_bins_file: `fraction` of the rank's split of the file (evenly
- *     spaced blocks; the reference samples 1 %). */
+ *     spaced blocks; the reference samples 1 %); world / rank as for
+ *     fk_ingest_file_range. */
 int fk_balance_bins(fk_ctx *ctx, const uint8_t *sample, size_t n);
 int fk_balance_bins_file(fk_ctx *ctx, const char *path, int32_t world, int32_t rank, double fraction);
 /* Host-only arithmetic of one exchange step.  sent[d * (2 * parts + 1) + i] is this
@@ -273,7 +276,7 @@ int fk_get_stats(fk_ctx *ctx, fk_stats *out);
  * One bucket through the wave-tier count kernel on `device`: the n keys
  * (k <= 32: one word each, n <= 512; 33 <= k <= 63: (hi, lo) pairs, n <= 256)
  * must lie in cells [c0, c1) of F cell bits (cell = top F bits of the 2k-bit
- * key); slots = table slots per bucket (768 / 1024, or 384 / 512 for k > 32).
+ * key); slots = table slots per bucket, the product's (768, or 384 for k > 32).
  * Writes the distinct keys ascending and their counts, *n_out of them.  Lets
  * tests drive adversarial buckets (every key in one rank group, keys over all
  * groups) that FASTA inputs cannot aim at. */

@@ -84,6 +84,21 @@ JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_ingestFileRange(JNIE
     if (rc != FK_OK) throw_fk(env, rc);
 }
 
+/* def balanceBinsFile(h, path, world, rank, fraction): Unit -- useCustomPartitioner (SBKC:1023-1026,
+ * MultiprocessorSchedulingPartitioner.scala:35-69): `fraction` of this rank's split mapped (never
+ * exchanged), the per-bin k-mer totals summed over the ranks, the LPT placement installed for the
+ * job's exchange; collective, before ingestFileRange */
+JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_balanceBinsFile(JNIEnv *env, jobject self, jlong h,
+                                                                           jstring path, jint world, jint rank,
+                                                                           jdouble fraction) {
+    (void)self;
+    const char *p = (*env)->GetStringUTFChars(env, path, NULL);
+    if (!p) return;
+    const int rc = fk_balance_bins_file(ctx_of(h), p, world, rank, fraction);
+    (*env)->ReleaseStringUTFChars(env, path, p);
+    if (rc != FK_OK) throw_fk(env, rc);
+}
+
 /* def finish(h): Unit -- map and count (one rank); with a communicator the last piece, the
  * exchange with the other ranks and the count of this rank's bins (collective) */
 JNIEXPORT void JNICALL Java_skc_gpu_NativeKmerCounter_00024_finish(JNIEnv *env, jobject self, jlong h) {

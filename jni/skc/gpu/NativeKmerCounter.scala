@@ -20,6 +20,7 @@ object NativeKmerCounter {
                      nRanks: Int, rank: Int, device: Int): Long
   @native def ingest(h: Long, fasta: java.nio.ByteBuffer, n: Long, last: Boolean): Unit
   @native def ingestFileRange(h: Long, path: String, world: Int, rank: Int, window: Long): Unit
+  @native def balanceBinsFile(h: Long, path: String, world: Int, rank: Int, fraction: Double): Unit
   @native def finish(h: Long): Unit
   @native def commUniqueId(): Array[Byte]
   @native def commInit(h: Long, id: Array[Byte]): Unit
@@ -50,13 +51,18 @@ object NativeKmerCounter {
     * range with a header prefix and the k - 1 overlap -- and streams it in windows of `window`
     * bytes (any split size: no 2 GiB mapping limit).  The records move between the GPUs inside
     * ingest / finish (RCCL all-to-all over xGMI, the reduceByKey of :1034-1042); each rank writes
-    * the bin files of the bins it owns (bin % nRanks == rank) into the shared output directory. */
+    * the bin files of the bins it owns into the shared output directory: bin % nRanks == rank, or
+    * with configuration.useCustomPartitioner the LPT placement of the reference's partitioner
+    * (SBKC:1023-1026; MultiprocessorSchedulingPartitioner.scala:35-69) computed from a 1 % sample
+    * of every rank's split (sample(false, 0.01), SBKC:1024) before the job's input is read. */
   def executeJobRank(configuration: TestConfiguration, rank: Int, nRanks: Int, commId: Array[Byte],
                      device: Int = -1, window: Long = 1L << 28): Array[Long] = {
     val h = create(configuration.k, configuration.m, configuration.x, configuration.b,
       configuration.useHT, configuration.sequenceType, nRanks, rank, device)
     try {
       commInit(h, commId)
+      if (configuration.useCustomPartitioner)
+        balanceBinsFile(h, configuration.dataset, nRanks, rank, 0.01)
       ingestFileRange(h, configuration.dataset, nRanks, rank, window)
       finish(h)
       if (configuration.write) writeBins(h, configuration.outputDir)

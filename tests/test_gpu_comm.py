@@ -100,15 +100,12 @@ def assert_union_matches_oracle(ctxs, ref, ordered=True, owner=None):
         assert np.array_equal(cnt, rcnt), f"counts differ in bin {b}"
 
 
-@pytest.fixture(params=[1, 0], ids=["staged", "merge"])
-def small_pieces(monkeypatch, request):
+@pytest.fixture
+def small_pieces(monkeypatch):
     # 256 KB H2D segments and 512 KB pieces: a few MB of input crosses several pieces; the
-    # received segments either expanded as staged pieces and counted once (1, the default for
-    # k <= 32) or counted per step and merged (0)
+    # received segments are expanded as staged pieces while later steps move, and counted once
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
-    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(request.param))
-    return request.param
 
 
 @pytest.mark.parametrize("world,use_ht,feed", [(2, False, "pinned"), (3, False, "bytes"), (8, False, "pinned"),
@@ -121,7 +118,7 @@ def test_local_exchange_vs_oracle(small_pieces, world, use_ht, feed):
     assert sum(s["kmers"] for s in st) == ref.total_kmers
     if feed == "pinned":  # pieces went out during the ingest, then the last piece (and closing steps)
         assert all(s["xch_steps"] >= (3 if world == 2 else 2) for s in st)
-        if world == 2 and not use_ht:  # earlier steps were counted while later ones moved, then merged
+        if world == 2 and not use_ht:  # earlier steps were staged while later ones moved
             assert all(s["pieces_counted"] >= 2 for s in st)
     assert sum(s["xch_bytes_sent"] for s in st) == sum(s["xch_bytes_received"] for s in st) > 0
     assert_union_matches_oracle(ctxs, ref, ordered=not use_ht)
@@ -396,3 +393,56 @@ def test_local_exchange_size_aware_placement(small_pieces, tmp_path, use_ht, k, 
     lpt = max(km[owner == r].sum() for r in range(G))
     default = max(km[np.arange(2048) % G == r].sum() for r in range(G))
     assert lpt <= default * 1.02, (lpt, default)
+
+
+def test_local_exchange_rank_closed_right_after_finish(small_pieces):
+    # a rank destroyed right after fk_finish while its peer may still be in the job's
+    # last step (waiting on the closed rank's events, copying out of its send buffer) -- the peer's
+    # result stays exact.  Rank 1 holds a fraction of rank 0's input, so rank 0 takes the
+    # closing steps; repeated so both arrival orders at the last barrier occur.
+    fasta = fk.synth_fasta(30_000, 100, 400_000, seed=0xEC)
+    ref = oracle.OracleResult(fasta, 28, 10, 2048)
+    cut = 114 * 26_000
+    shards = [fasta[:cut], fasta[cut:]]
+    for _ in range(4):
+        ctxs = [fk.KmerCounter(28, 10, 3, 2048, n_ranks=2, rank=r) for r in range(2)]
+        fk.comm_init_local(ctxs)
+        errs = [None, None]
+
+        def work(r):
+            try:
+                ctxs[r].ingest(shards[r])
+                ctxs[r].finish()
+                if r == 1:
+                    ctxs[1].close()
+            except Exception as e:  # noqa: BLE001
+                errs[r] = e
+        th = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+        [t.start() for t in th]
+        [t.join(timeout=120) for t in th]
+        assert not any(t.is_alive() for t in th)
+        assert errs == [None, None], errs
+        sizes = ctxs[0].bin_sizes()
+        for b in range(0, 2048, 2):
+            assert sizes[b] == ref.bin_size(b)
+            if b % 64 == 0 and sizes[b]:
+                _, lo, cnt = counter_arrays(ctxs[0], b)
+                _, rlo, rcnt = ref.bin_arrays(b)
+                assert np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
+        ctxs[0].close()
+
+
+def test_split_of_another_rank_is_refused(tmp_path):
+    # with a communicator the file split must be the context's own (world, rank)
+    path = tmp_path / "in.fa"
+    path.write_bytes(fk.synth_fasta(2_000, 100, 50_000, seed=0xED))
+    ctxs = [fk.KmerCounter(28, 10, 3, 2048, n_ranks=2, rank=r) for r in range(2)]
+    fk.comm_init_local(ctxs)
+    with pytest.raises(fk.FastKmerError) as e:
+        ctxs[0].ingest_file_range(str(path), world=2, rank=1)
+    assert e.value.code == -1 and "split 1 of 2" in str(e.value)
+    with pytest.raises(fk.FastKmerError) as e:
+        ctxs[1].balance_bins_file(str(path), world=3, rank=1)
+    assert e.value.code == -1
+    for c in ctxs:
+        c.close()

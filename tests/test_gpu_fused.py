@@ -42,22 +42,19 @@ def _fasta(rng: random.Random, n_rec: int, min_len: int, max_len: int, width=Non
     return "".join(out).encode()
 
 
-def _run(fasta, k, m, x, B, use_ht=False, nt=None, monkeypatch=None, sequence_type=0):
-    if nt is not None:
-        monkeypatch.setenv("FASTKMER_FUSED_NT", str(nt))
+def _run(fasta, k, m, x, B, use_ht=False, sequence_type=0):
     kc = fk.KmerCounter(k, m, x, B, use_ht, sequence_type)
     kc.ingest(fasta)
     kc.finish()
     return kc
 
 
-@pytest.mark.parametrize("nt", [256, 512])
 @pytest.mark.parametrize("k,m,x,B", CONFIGS)
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_fused_random_vs_oracle(monkeypatch, nt, k, m, x, B, seed):
-    rng = random.Random(1000 * seed + k + nt)
+def test_fused_random_vs_oracle(k, m, x, B, seed):
+    rng = random.Random(1000 * seed + k + 512)
     fasta = _fasta(rng, 3000, 1, 400, noise=0.01)
-    kc = _run(fasta, k, m, x, B, nt=nt, monkeypatch=monkeypatch)
+    kc = _run(fasta, k, m, x, B)
     st = kc.stats()
     assert st["fused_map"] == 1, ("the fused kernel should place this input", st["fused_fallback"])
     ref = oracle.OracleResult(fasta, k, m, B)
@@ -65,12 +62,11 @@ def test_fused_random_vs_oracle(monkeypatch, nt, k, m, x, B, seed):
     assert_same_as_oracle(kc, ref)
 
 
-@pytest.mark.parametrize("nt", [256, 512])
-def test_fused_short_reads_both_modes(monkeypatch, nt):
+def test_fused_short_reads_both_modes():
     fasta = fk.synth_fasta(40_000, 100, 500_000, seed=77)
     ref = oracle.OracleResult(fasta, 28, 10, 2048)
     for use_ht in (False, True):
-        kc = _run(fasta, 28, 10, 3, 2048, use_ht, nt=nt, monkeypatch=monkeypatch)
+        kc = _run(fasta, 28, 10, 3, 2048, use_ht)
         assert kc.stats()["fused_map"] == 1
         assert_same_as_oracle(kc, ref, ordered=not use_ht)
         kc.close()
@@ -94,8 +90,7 @@ def test_fused_matches_two_kernel_path_records(monkeypatch):
 @pytest.mark.parametrize("case", ["long_header", "long_line", "junk_first", "one_base_lines", "crlf",
                                   "header_across_tiles", "header_at_chunk_start", "tiny", "empty",
                                   "no_newline_end", "blank_lines"])
-@pytest.mark.parametrize("nt", [256, 512])
-def test_fused_edge_inputs_vs_oracle(monkeypatch, case, nt):
+def test_fused_edge_inputs_vs_oracle(case):
     rng = random.Random(sum(case.encode()))
     expect_fused = True
     if case == "long_header":  # a 10 kB header line over bytes ~59.5k-69.5k: the tiles starting at
@@ -135,7 +130,7 @@ def test_fused_edge_inputs_vs_oracle(monkeypatch, case, nt):
     else:  # the last line has no trailing newline
         fasta = _fasta(rng, 500, 50, 300).rstrip(b"\n")
     for k, m, x, B in CONFIGS:
-        kc = _run(fasta, k, m, x, B, nt=nt, monkeypatch=monkeypatch)
+        kc = _run(fasta, k, m, x, B)
         ref = oracle.OracleResult(fasta, k, m, B)
         st = kc.stats()
         assert st["kmers"] == ref.total_kmers

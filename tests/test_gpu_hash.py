@@ -42,18 +42,13 @@ def test_ht_two_word_lds_tables_vs_oracle(k, m, B):
             assert st["ht_rounds"] > 1
 
 
-@pytest.mark.parametrize("k,m,B,thr,huge", [(55, 12, 64, 600, 0), (63, 15, 64, 1500, 0), (55, 12, 1, 2000, 0),
-                                              (55, 12, 1, 0, 0), (55, 12, 64, 400, 900), (55, 12, 1, 1000, 3000),
-                                              (28, 10, 64, 500, 0), (28, 10, 1, 3000, 0), (28, 10, 1, 0, 0)])
-def test_ht_heavy_group_tables_vs_oracle(monkeypatch, k, m, B, thr, huge):
+@pytest.mark.parametrize("k,m,B,thr", [(55, 12, 64, 600), (63, 15, 64, 1500), (55, 12, 1, 2000), (55, 12, 1, 0),
+                                        (55, 12, 64, 400)])
+def test_ht_heavy_group_tables_vs_oracle(monkeypatch, k, m, B, thr):
     # k > 32 with FASTKMER_HT_BIG: groups of more than thr k-mers take the 6144-slot tables
     # (k_ht_combine128<false, 1024, 6144> over the device-listed heavy groups), the rest the
-    # 2048-slot ones; B = 1 still spills past the big tables; thr = 0: every group in 2048 slots;
-    # FASTKMER_HT_HUGE: groups of thr..huge k-mers take the 3072-slot tables, larger ones 6144
-    # (k <= 32: FASTKMER_HT_BIG64, the 8192-slot 64-bit tables)
+    # 2048-slot ones; B = 1 still spills past the big tables; thr = 0: every group in 2048 slots
     monkeypatch.setenv("FASTKMER_HT_BIG", str(thr))
-    monkeypatch.setenv("FASTKMER_HT_BIG64", str(thr))
-    monkeypatch.setenv("FASTKMER_HT_HUGE", str(huge))
     fasta = fk.synth_fasta(40_000, 150, 20_000_000, seed=0xB3 + k + B)
     with fk.KmerCounter(k, m, 3, B, use_ht=True) as kc:
         kc.ingest(fasta)

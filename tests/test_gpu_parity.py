@@ -447,14 +447,12 @@ def test_block_and_big_tiers_vs_oracle(monkeypatch):
     assert_same_as_oracle(kc, ref)
 
 
-@pytest.mark.parametrize("slots", ["768", "1024"])
 @pytest.mark.parametrize("k,m", [(28, 10), (55, 12)])
-def test_wave_tables_of_distinct_keys_vs_oracle(monkeypatch, slots, k, m):
+def test_wave_tables_of_distinct_keys_vs_oracle(k, m):
     # reads of a 3 Gbp virtual genome: nearly every k-mer is distinct, so the
     # wave buckets (512 keys; 256 two-word keys for k > 32) fill their tables
     # with as many distinct keys (2/3 of the 768 / 384 slots: the longest
     # probe runs)
-    monkeypatch.setenv("FASTKMER_WAVE_SLOTS", slots)
     fasta = fk.synth_fasta(100_000, 100, 3_000_000_000, seed=61)
     kc = run_counter(fasta, k, m, 3, 64)
     ref = oracle.OracleResult(fasta, k, m, 64)
@@ -463,13 +461,11 @@ def test_wave_tables_of_distinct_keys_vs_oracle(monkeypatch, slots, k, m):
 
 
 @pytest.mark.parametrize("env", [
-    {"FASTKMER_COUNT_MODE": "0"},                                   # one workgroup per <= 2048-key bucket
-    {"FASTKMER_EXPAND_LEVELS": "1"},                                # one-level write-combined scatter
-    {"FASTKMER_EXPAND_LEVELS": "1", "FASTKMER_DEBUG_SCATTER": "0"},  # plain scatter
-    {"FASTKMER_WAVE_CAP": "256", "FASTKMER_WAVE_BPW": "1"},
-    {"FASTKMER_WAVE_CAP": "128", "FASTKMER_WAVE_BPW": "2", "FASTKMER_DEBUG_CELL_TARGET": "64"},
+    {"FASTKMER_DEBUG_LARGE_BUCKETS": "1"},                           # every bucket through the streaming path
+    {"FASTKMER_DEBUG_CELL_TARGET": "64"},                            # small cells: many small buckets
+    {"FASTKMER_DEBUG_CELL_TARGET": "2600"},                          # large cells: block and big tiers
     {"FASTKMER_X2_L1": "1024"},                                      # 1024-record level-1 batches
-    {"FASTKMER_WAVE_SLOTS": "1024"},                                 # 2 slots per key in the wave tables
+    {"FASTKMER_FUSED": "0"},                                         # the two-kernel map
 ])
 def test_count_variants_identical(monkeypatch, env):
     # every count-stage variant gives the default path's result, bit for bit
@@ -485,7 +481,7 @@ def test_count_variants_identical(monkeypatch, env):
         assert np.array_equal(kb, ka) and np.array_equal(cb, ca)
 
 
-@pytest.mark.parametrize("case", ["long_lines", "text_before_header", "forced_lookback"])
+@pytest.mark.parametrize("case", ["long_lines", "text_before_header", "wrapped"])
 def test_parse_line_lookback_paths_vs_oracle(monkeypatch, case):
     # the parse finds the line holding each tile start by reading back 4 KB;
     # lines longer than that (sequence or header) and text before the first
@@ -498,8 +494,8 @@ def test_parse_line_lookback_paths_vs_oracle(monkeypatch, case):
                  + random_fasta(rng, 200, 50, 150))
     elif case == "text_before_header":
         fasta = b"ACGTACGTTTGACCAGGGTACCA\nGGGTTTACCAGT\n" + random_fasta(rng, 500, 50, 300)
-    else:
-        monkeypatch.setenv("FASTKMER_PARSE_LOOKBACK", "1")
+    else:  # wrapped lines through the two-kernel path's scan variant
+        monkeypatch.setenv("FASTKMER_FUSED", "0")
         fasta = random_fasta(rng, 2000, 50, 300, wrap=61)
     for k, m in ((28, 10), (55, 12)):
         kc = run_counter(fasta, k, m, 3, 512)
@@ -556,4 +552,59 @@ def test_grouped_exchange_in_one_process_matches_oracle(k, m, B, use_ht):
             if use_ht:
                 o = np.lexsort((lo, hi))
                 hi, lo, cnt = hi[o], lo[o], cnt[o]
+            assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
+
+
+@pytest.mark.parametrize("k,m,B", [(28, 10, 2048), (55, 12, 8192)])
+def test_grouped_emit_with_owners_set_after_map(k, m, B):
+    # the caller-driven custom-partitioner flow: fk_set_grouped_emit, fk_map,
+    # fk_map_bin_kmers, LPT over the summed sizes, fk_set_bin_owners -- which must keep the mapped
+    # records and recompute their (owner, local bin) parts -- then fk_map_emit / fk_reduce_grouped
+    fasta = fk.synth_fasta(18_000, 150 if k > 32 else 100, 400_000, seed=83)
+    G = 3
+    rec = len(fasta) // 18_000
+    shards = [fasta[r * rec * 6000:(r + 1) * rec * 6000] for r in range(G)]
+    ranks = [fk.KmerCounter(k, m, 3, B, False, 0, n_ranks=G, rank=r) for r in range(G)]
+    import torch
+    sizes = np.zeros(ranks[0].num_bins, dtype=np.uint64)
+    for r in range(G):
+        ranks[r].set_grouped_emit(True)
+        ranks[r].ingest(shards[r])
+        ranks[r].map()
+        sizes += ranks[r].map_bin_kmers()
+    owner = fk.lpt_owners(sizes, G)
+    assert (owner != np.arange(len(owner)) % G).any()  # not the default placement
+    sends = []
+    for r in range(G):
+        counts = ranks[r].set_bin_owners(owner)
+        prec, pkm = ranks[r].map_part_counts()
+        parts = prec.shape[1]
+        assert sum(counts) > 0 and [int(x) for x in prec.sum(axis=1)] == counts
+        buf = torch.empty(max(sum(counts), 1) * ranks[r].record_bytes, dtype=torch.uint8, device="cuda")
+        ranks[r].map_emit(buf.data_ptr(), max(sum(counts), 1))
+        torch.cuda.synchronize()
+        sends.append((buf, counts, prec, pkm))
+    rb = ranks[0].record_bytes
+    for dst in range(G):
+        pieces, seg_rec, seg_km = [], [], []
+        for src in range(G):
+            buf, counts, prec, pkm = sends[src]
+            off = sum(counts[:dst])
+            pieces.append(buf[off * rb:(off + counts[dst]) * rb])
+            seg_rec.append(prec[dst])
+            seg_km.append(pkm[dst])
+        recv = torch.cat(pieces)
+        ranks[dst].reduce_grouped(recv.data_ptr(), recv.numel() // rb, np.stack(seg_rec), np.stack(seg_km))
+        torch.cuda.synchronize()
+    ref = oracle.OracleResult(fasta[:G * rec * 6000], k, m, B)
+    total = np.zeros(ref.nbins, dtype=np.int64)
+    for dst in range(G):
+        got = ranks[dst].bin_sizes().astype(np.int64)
+        assert all(got[b] == 0 for b in range(ref.nbins) if owner[b] != dst)
+        total += got
+    assert np.array_equal(total, ref.bin_sizes())
+    for b in range(0, ref.nbins, 41):
+        if ref.bin_size(b):
+            hi, lo, cnt = counter_arrays(ranks[owner[b]], b)
+            rhi, rlo, rcnt = ref.bin_arrays(b)
             assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)

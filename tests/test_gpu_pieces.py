@@ -1,20 +1,15 @@
-"""Pieces of a job counted while the FASTA is still landing, through the C-ABI.
+"""Staged pieces of a job, through the C-ABI.
 
-Two modes (FASTKMER_PIECE_MODE): 1, staged (the default for k <= 32): every piece is
-partitioned and expanded into its own key array, and fk_finish counts the job's
-buckets once over all the pieces' keys; 0, per-piece counts merged (fk_merge.inc,
-the k > 32 path), described below.
-
-While the FASTA is still being copied in, every landed piece of it is
-counted on its own (the sorted count of extractKXmers, SBKC:540-597, on the
-piece's records) and merged into the running result of the earlier pieces
-bin by bin, adding the counts of equal k-mers; fk_finish counts and merges
-the last piece.  A bin's multiset is
-the sum of its pieces' multisets, so the merged result must be bit-exact
-against the CPU oracle over the whole input -- checked here at sizes the
-oracle finishes quickly, with the pieces made small (FASTKMER_PIECE_BYTES) so
-that inputs of a few MB cross many of them, for key distributions that
-differ from piece to piece.
+While the FASTA is still being copied in, every landed piece of it is partitioned
+(the bin grouping of reduceByKey, SBKC:1035) and expanded into canonical k-mers in
+its own key array; fk_finish expands the last piece and counts the job's buckets
+once over all the pieces' keys (the sorted count of extractKXmers, SBKC:540-597).
+A bin's multiset is the sum of its pieces' multisets, so the result must be
+bit-exact against the CPU oracle over the whole input -- checked here at sizes
+the oracle finishes quickly, with the pieces made small (FASTKMER_PIECE_BYTES)
+so that inputs of a few MB cross several of them, for key distributions that
+differ from piece to piece.  The hash count and k = 64 count the whole input
+after the last byte.
 """
 import numpy as np
 import pytest
@@ -26,15 +21,10 @@ from test_gpu_parity import assert_same_as_oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 0, 2], ids=["staged", "merge", "staged-precount"])
-def small_pieces(monkeypatch, request):
-    # 2: staged with the pre-count forced (FASTKMER_PRECOUNT=1): the first two pieces' buckets are
-    # counted while the rest lands, the final count merges them with the later pieces' k-mers
+@pytest.fixture
+def small_pieces(monkeypatch):
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
-    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(min(request.param, 1)))
-    monkeypatch.setenv("FASTKMER_PRECOUNT", "1" if request.param == 2 else "0")
-    return request.param
 
 
 def count_pinned(fasta, k, m, B=2048, use_ht=False, seq=0, repeat=1):
@@ -54,8 +44,7 @@ def test_piece_counts_merge_vs_oracle(small_pieces, k, m, read_len, B):
     fasta = fk.synth_fasta(40_000 if read_len == 100 else 25_000, read_len, 1_000_000, seed=0xA1 + k)
     kc = count_pinned(fasta, k, m, B, repeat=2)  # twice: the piece buffers are reused by the second job
     st = kc.stats()
-    assert st["pieces_counted"] >= 4 and st["fused_map"] == 1
-    assert st["precounted"] == (1 if small_pieces == 2 and k <= 32 else 0)
+    assert st["pieces_counted"] == 4 and st["fused_map"] == 1
     ref = oracle.OracleResult(fasta, k, m, B)
     assert st["kmers"] == ref.total_kmers and st["distinct"] == ref.distinct
     assert_same_as_oracle(kc, ref)
@@ -64,8 +53,7 @@ def test_piece_counts_merge_vs_oracle(small_pieces, k, m, read_len, B):
 def test_piece_counts_disjoint_and_skewed_pieces(small_pieces):
     # piece key distributions that share nothing: reads of two unrelated genomes one after the
     # other, a stretch of one repeated read (a piece holding few keys, with huge counts), and
-    # a low-complexity stretch -- the splitters of a bin come from one piece only, so segments
-    # of the others take several merge rounds
+    # a low-complexity stretch -- a bucket's keys come from one piece only, or from all of them
     a = fk.synth_fasta(12_000, 100, 300_000, seed=0xA2)
     b = fk.synth_fasta(12_000, 100, 300_000, seed=0xA3, first_read=12_000)
     rep = b"".join(b">r%010d\n" % i + b"ACGTTGCAAGGCTTACCGATCGGATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAGCATG"
@@ -78,8 +66,8 @@ def test_piece_counts_disjoint_and_skewed_pieces(small_pieces):
 
 
 def test_piece_counts_piece_without_kmers(small_pieces):
-    # pieces that hold no k-mer at all (reads of N only) between pieces that do: the staged path
-    # skips them (no key array, no piece), the merge path counts them as empty
+    # pieces that hold no k-mer at all (reads of N only) between pieces that do: they are skipped
+    # (no key array, no piece)
     a = fk.synth_fasta(8_000, 100, 300_000, seed=0xA7)
     nn = b"".join(b">n%d\n" % i + b"N" * 100 + b"\n" for i in range(20_000))
     b = fk.synth_fasta(8_000, 100, 300_000, seed=0xA8, first_read=8_000)
@@ -99,8 +87,8 @@ def test_piece_counts_long_sequence(small_pieces):
 
 
 def test_piece_counts_fallback_counts_whole_input(small_pieces):
-    # a 40 KB line after several pieces were counted: the fused map hands the input back, the
-    # piece results are dropped and the whole input is counted by the two-kernel path
+    # a 40 KB line after several pieces were staged: the fused map hands the input back, the
+    # staged pieces are dropped and the whole input is counted by the two-kernel path
     fasta = fk.synth_fasta(30_000, 100, 600_000, seed=0xA4)
     cut = len(fasta) * 3 // 4 // 114 * 114
     fasta = fasta[:cut] + b">" + b"h" * 40_000 + b"\n" + b"ACGT" * 40 + b"\n" + fasta[cut:]
@@ -111,35 +99,28 @@ def test_piece_counts_fallback_counts_whole_input(small_pieces):
 
 
 def test_piece_counts_hash_mode_counts_once(small_pieces):
-    # useHT=1 (table order does not merge): the whole input is counted in fk_finish
+    # useHT=1: the whole input is counted in fk_finish
     fasta = fk.synth_fasta(20_000, 100, 400_000, seed=0xA5)
     kc = count_pinned(fasta, 28, 10, use_ht=True)
     assert kc.stats()["pieces_counted"] == 0
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048), ordered=False)
 
 
-@pytest.mark.parametrize("mode", [1, 0], ids=["staged", "merge"])
-def test_piece_counts_many_small_pieces(monkeypatch, mode):
-    # merge: dozens of pieces, each merged into the running result as it is counted; staged: the
-    # first pieces expanded as they land (at most STAGE_MAXP pieces), the rest the last piece
+def test_piece_counts_many_small_pieces(monkeypatch):
+    # 64 KB pieces of a 3.4 MB job: the first pieces expanded as they land (at most STAGE_MAXP - 1
+    # before fk_finish), the rest is the last piece
     monkeypatch.setenv("FASTKMER_INGEST_SEG", str(64 << 10))
     monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(64 << 10))
-    monkeypatch.setenv("FASTKMER_PIECE_MODE", str(mode))
     fasta = fk.synth_fasta(30_000, 100, 500_000, seed=0xA6)
     kc = count_pinned(fasta, 28, 10, repeat=2)
-    if mode:
-        assert kc.stats()["pieces_counted"] == 4
-    else:
-        assert kc.stats()["pieces_counted"] >= 20
+    assert kc.stats()["pieces_counted"] == 4
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
 
 
-@pytest.mark.parametrize("cuts,one_level,chunks,pre", [("0.45,0.7,0.85", "0.2", 0, "0"), ("0.3", "0", 0, "0"),
-                                                       ("0.2,0.25,0.97", "0.5", 0, "0"), ("0.45,0.7,0.85", "0.2", 7, "0"),
-                                                       ("0.45,0.7,0.85", "0", 0, "1"), ("0.45,0.7,0.85", "0", 7, "1")])
-def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks, pre):
+@pytest.mark.parametrize("cuts,chunks", [("0.45,0.7,0.85", 0), ("0.3", 0), ("0.2,0.25,0.97", 0), ("0.4,0.7,0.9", 7)])
+def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, chunks):
     # a 1 GB job in one fk_ingest call (pinned): staged pieces at the job-size cuts (the
-    # bench's path) against the same job counted whole on the device (FASTKMER_PIECE_COUNT=0),
+    # bench's path) against the same job counted whole from HBM (fk_ingest_device: no pieces),
     # every bin's keys and counts equal; a sampled slice of bins against the oracle is in
     # test_gpu_write; here both GPU paths must agree on all 2048 bins (a piece ends at its cut once it
     # holds >= 128 MB: "0.2,0.25,0.97" cuts at 0.2, ~0.33 and 0.97)
@@ -151,8 +132,6 @@ def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks, pre)
     host.copy_(dev)
     torch.cuda.synchronize()
     monkeypatch.setenv("FASTKMER_PIECE_CUTS", cuts)
-    monkeypatch.setenv("FASTKMER_STAGED_ONE_LEVEL", one_level)  # pieces below this job fraction: one pass
-    monkeypatch.setenv("FASTKMER_PRECOUNT", pre)  # 1: the first two pieces counted while the rest lands
     a = fk.KmerCounter(28, 10, 3, 2048)
     if chunks:  # a streamed job: fk_ingest_reserve announces its size, the cuts follow it
         a.reserve(host.numel())
@@ -164,8 +143,6 @@ def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, one_level, chunks, pre)
     a.finish()
     st = a.stats()
     assert st["pieces_counted"] == cuts.count(",") + 2
-    assert st["precounted"] == int(pre)
-    monkeypatch.setenv("FASTKMER_PIECE_COUNT", "0")
     b = fk.KmerCounter(28, 10, 3, 2048)
     b.ingest_device(dev.data_ptr(), dev.numel())
     b.finish()
