@@ -59,7 +59,8 @@ class fk_stats(ctypes.Structure):
                                        ("ms_exchange_tail", ctypes.c_double),
                                        ("pieces_counted", ctypes.c_uint64), ("ms_merge", ctypes.c_double),
                                        ("precounted", ctypes.c_uint64), ("block_buckets", ctypes.c_uint64), ("big_buckets", ctypes.c_uint64),
-                                       ("ht_big_groups", ctypes.c_uint64)]
+                                       ("ht_big_groups", ctypes.c_uint64), ("split_buckets", ctypes.c_uint64),
+                                       ("sub_buckets", ctypes.c_uint64)]
 
 COMM_ID_BYTES = 128
 

@@ -322,6 +322,7 @@ struct fk_ctx {
     DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_total;
     DevBuf table_off, tkeys, tstate, tcounts;
+    DevBuf sp_base, sp_keys, sp_subs, sp_par, sp_uniq, sp_fb;  // heavy buckets split into sub-buckets
     ScanWorkspace ws;
     // results
     bool have_result = false;
@@ -613,7 +614,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
-                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts};
+                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts,
+                      &c->sp_base, &c->sp_keys, &c->sp_subs, &c->sp_par, &c->sp_uniq, &c->sp_fb};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -1599,11 +1601,13 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         FK_TRY(ensure(*B.tier_list, nbuckets * 8));
         uint32_t *lists = B.tier_list->as<uint32_t>();
         HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, cap,
-                                    B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(), s));
-        // the tier sizes go to pinned memory right behind the tier kernel: the host waits for that
-        // copy, not for the wave tier queued after it, before it queues the block tiers
-        if (c->pin_tier.ensure(16)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-        HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 8, hipMemcpyDeviceToHost, s));
+                                    B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(),
+                                    c->misc.as<unsigned long long>() + 3, s));
+        // the tier sizes (and the listed buckets' keys) go to pinned memory right behind the tier
+        // kernel: the host waits for that copy, not for the wave tier queued after it, before it
+        // queues the heavier tiers
+        if (c->pin_tier.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
+        HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipEventRecord(c->tier_ev, s));
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
@@ -1615,20 +1619,76 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                                 okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                                 B.bucket_unique->as<uint64_t>(), s));
         HIP_TRY(hipEventSynchronize(c->tier_ev));
-        uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
+        const uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
+        const uint64_t listed_keys = c->pin_tier.as<uint64_t>()[3];
         htrace("sorted: tiers read");
         c->stats.block_buckets = ntier[0];
         c->stats.big_buckets = ntier[1];
         hipStream_t ts = s;
-        if (ntier[0] && c->KW == 1) {
-            HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k,
-                                          okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                          B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1,
-                                          cap, 99, lists, ts));
-        } else if (ntier[0]) {
+        uint64_t nlarge = 0;
+        if (c->KW == 1 && (ntier[0] || ntier[1])) {
+            // 64-bit keys: the buckets above the wave tier split into wave-sized sub-buckets by the key
+            // bits below their common prefix, counted by the wave tier and joined back; the buckets
+            // with a sub-bucket too large for a wave keep the block / big-table kernels
+            const uint32_t nl = ntier[0] + ntier[1];
+            const uint64_t maxsub = listed_keys / 64 + nl + 64;  // 2^b < 2 n / SPL_KEYS sub-buckets per bucket
+            FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
+            FK_TRY(ensure(c->sp_keys, listed_keys * 8));
+            FK_TRY(ensure(c->sp_subs, maxsub * sizeof(SubBucket)));
+            FK_TRY(ensure(c->sp_par, (uint64_t)nl * sizeof(SplitParent)));
+            FK_TRY(ensure(c->sp_uniq, maxsub * 8));
+            FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
+            const uint32_t *l1 = lists + nbuckets;
+            uint32_t *fb = c->sp_fb.as<uint32_t>();
+            unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
+            HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                                        c->sp_base.as<uint64_t>(), s));
+            HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
+                                      c->sp_base.as<uint64_t>() + nl, c->ws, s));
+            HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                                          c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
+                                          c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb, fb + nl,
+                                          cap, s));
+            HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipEventRecord(c->tier_ev, s));
+            HIP_TRY(hipEventSynchronize(c->tier_ev));
+            const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
+            const uint32_t nsub = sc[0], nfb0 = sc[1], nfb1 = sc[2];
+            htrace("sorted: split counts read");
+            if (nsub > maxsub) return set_err(FK_E_DEVICE, "bucket split: %u sub-buckets of at most %llu", nsub,
+                                              (unsigned long long)maxsub);
+            HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
+                                            okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                            c->sp_uniq.as<uint64_t>(), s));
+            HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                                       c->sp_par.as<SplitParent>(), c->sp_subs.as<SubBucket>(),
+                                       c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                       B.bucket_unique->as<uint64_t>(), s));
+            c->stats.split_buckets = nl - nfb0 - nfb1;
+            c->stats.sub_buckets = nsub;
+            if (nfb0)
+                HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nfb0, k, okb.as<uint64_t>(),
+                                              B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                              c->misc.as<unsigned long long>() + 1, cap, 99, fb, s));
+            if (nfb1) {
+                // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
+                HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfb1, k, okb.as<uint64_t>(),
+                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                                  c->misc.as<unsigned long long>() + 2, fb + nl, s));
+                HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+            }
+            if (nlarge) {
+                FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+                HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), nfb1, k,
+                                                 c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
+                                                 B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                                 fb + nl, s));
+            }
+        } else if (ntier[0] || ntier[1]) {
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
             // 768-slot table (a cell of a large bin, ~340 keys at configs[3]'s per-GPU bins), the rest
-            // the LDS radix sort
+            // the LDS radix sort; buckets above the block tier the streaming path
             HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                     okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                                     B.bucket_unique->as<uint64_t>(), ts));
@@ -1636,23 +1696,14 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                        B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, ts, WAVE128_MID_CAP));
-        }
-        uint64_t nlarge = ntier[1];
-        if (ntier[1] && c->KW == 1 && !c->force_large) {
-            // buckets above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
-            HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), ntier[1], k,
-                                              okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                              B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 2,
-                                              lists + nbuckets, ts));
-            HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, ts));
-            HIP_TRY(hipStreamSynchronize(ts));
-        }
-        if (nlarge) {
-            FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
-            HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), ntier[1], k,
-                                             c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
-                                             B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                             lists + nbuckets, ts));
+            nlarge = ntier[1];
+            if (nlarge) {
+                FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+                HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), ntier[1], k,
+                                                 c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
+                                                 B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                                 lists + nbuckets, ts));
+            }
         }
         c->stats.oversize_buckets = nlarge;
     } else {

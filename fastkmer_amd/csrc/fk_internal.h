@@ -210,11 +210,41 @@ hipError_t launch_expand_hist_bin(int KW, const uint64_t *rec, const Chunk *chun
                                   hipStream_t s);
 hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbins, int F, uint32_t cap,
                                       int period_bits, uint32_t *flags, hipStream_t s);
+// lists[0, nb): buckets of wave_cap < n <= block_cap, lists[nb, 2 nb): above block_cap; counts[0] / [1]
+// their lengths; *listed_keys += their keys
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
-                               uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts, hipStream_t s);
+                               uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts,
+                               unsigned long long *listed_keys, hipStream_t s);
 hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                       const uint32_t *list, hipStream_t s);
+// heavy buckets (above the wave tier, k <= 32) split into wave-sized sub-buckets by the key bits
+// below their common prefix (k_bucket_split64), counted by the wave tier (k_sub_count64_wave) and
+// joined back into the bucket's output region (k_bucket_join)
+struct SubBucket {
+    uint64_t src;   // first key in the split copy (skeys)
+    uint64_t out;   // first output slot (the parent bucket's region of out_keys / out_counts)
+    uint64_t lo;    // every key lies in [lo, lo + 2^span)
+    uint32_t n, span;
+};
+struct SplitParent {
+    uint32_t first, nsub;  // sub-buckets [first, first + nsub) of the list; nsub = 0: not split
+};
+// sizes[i] = n of listed bucket i (list0 then list1)
+hipError_t launch_listed_sizes(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
+                               uint32_t n1, uint64_t *sizes, hipStream_t s);
+// counts[0] += sub-buckets, counts[1] / [2] += buckets left to the block / big path (fb0 / fb1: their
+// indices; a bucket of n <= block_cap goes to fb0)
+hipError_t launch_bucket_split64(const BucketSrc &src, const Bucket *buckets, const uint32_t *list0, uint32_t n0,
+                                 const uint32_t *list1, uint32_t n1, const uint64_t *sbase, uint64_t *skeys,
+                                 SubBucket *subs, SplitParent *parents, unsigned int *counts, uint32_t *fb0,
+                                 uint32_t *fb1, uint32_t block_cap, hipStream_t s);
+hipError_t launch_sub_count64_wave(const SubBucket *subs, uint64_t nsubs, const uint64_t *skeys, uint64_t *out_keys,
+                                   uint32_t *out_counts, uint64_t *sub_unique, hipStream_t s);
+hipError_t launch_bucket_join(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
+                              uint32_t n1, const SplitParent *parents, const SubBucket *subs,
+                              const uint64_t *sub_unique, uint64_t *out_keys, uint32_t *out_counts,
+                              uint64_t *bucket_unique, hipStream_t s);
 // dst[i] += src[i] (dst = src when `copy`)
 hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
 // skip_le: listed buckets of at most this many keys were counted by a wave tier (skipped)

@@ -89,6 +89,8 @@ typedef struct fk_stats {
     uint64_t block_buckets;    /* buckets above the wave tier of at most 2048 keys (mid wave tier, block kernel) */
     uint64_t big_buckets;      /* buckets above 2048 keys (the big-table kernel, then the large path) */
     uint64_t ht_big_groups;    /* useHT, k > 32: groups counted in the 6144-slot tables */
+    uint64_t split_buckets;    /* k <= 32: buckets above the wave tier split into wave-sized sub-buckets */
+    uint64_t sub_buckets;      /* ... into this many sub-buckets (the wave tier counted them) */
 } fk_stats;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

@@ -608,3 +608,34 @@ def test_grouped_emit_with_owners_set_after_map(k, m, B):
             hi, lo, cnt = counter_arrays(ranks[owner[b]], b)
             rhi, rlo, rcnt = ref.bin_arrays(b)
             assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
+
+
+@pytest.mark.parametrize("k,m,staged", [(28, 10, False), (32, 11, False), (28, 10, True), (21, 7, True)])
+def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged):
+    # buckets above the wave tier (cells of a few thousand keys, FASTKMER_DEBUG_CELL_TARGET) split into
+    # wave-sized sub-buckets by the key bits below their common prefix, counted by the wave tier and
+    # joined back in place -- from one key array and from staged pieces (a pinned ingest in 512 KB
+    # pieces); k = 32 keys use all 64 bits; repeated reads leave sub-buckets too large for a wave, which
+    # keep the block / big-table path
+    monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", "2600")
+    if staged:
+        monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
+        monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
+    rep = b"".join(b">q%d\n" % i + b"ACGTTGCAAGGCTTACCGATCGGATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAG"
+                   b"CATGCATGCATCGACGTAGCATCG\n" for i in range(3_000))
+    fasta = fk.synth_fasta(60_000, 100, 3_000_000_000, seed=0xC1 + k) + rep
+    if staged:
+        import torch
+        host = torch.frombuffer(bytearray(fasta), dtype=torch.uint8).pin_memory()
+        kc = fk.KmerCounter(k, m, 3, 16)
+        kc.ingest_ptr(host.data_ptr(), host.numel())
+        kc.finish()
+        assert kc.stats()["pieces_counted"] == 4
+    else:
+        kc = run_counter(fasta, k, m, 3, 16)
+    st = kc.stats()
+    assert st["split_buckets"] > 100 and st["sub_buckets"] > 8 * st["split_buckets"], st
+    assert st["split_buckets"] < st["block_buckets"] + st["big_buckets"], st  # the repeats fall back
+    ref = oracle.OracleResult(fasta, k, m, 16, threads=4)
+    assert st["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref)
