@@ -306,6 +306,7 @@ struct fk_ctx {
     DevBuf lh_parents, lh_parents2, lh_plan, lh_suboff, lh_part, lh_glist;  // spill rounds: parents, their plan, sub-ranges
     double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
     uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG (test hook): k > 32, groups of more k-mers take 6144-slot tables
+    int ht_groups = 0;            // FASTKMER_HT_GROUPS=1: useHT on the (bin, signature hash) group tables (A/B)
     int lh_probe = 0;             // FASTKMER_LH_PROBE (-DFK_PROBES): stop the combine kernel after a phase
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
@@ -540,6 +541,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *v = env("FASTKMER_X2_L1")) c->x2_l1 = atoi(v);
     if (const char *v = env("FASTKMER_FUSED")) c->fused = atoi(v);
     if (const char *v = env("FASTKMER_HT_BIG")) c->lh_big_thr = (uint32_t)strtoul(v, nullptr, 10);
+    if (const char *v = env("FASTKMER_HT_GROUPS")) c->ht_groups = atoi(v);
 #ifdef FK_PROBES
     if (const char *v = env("FASTKMER_DEBUG_PHASE")) c->dbg_phase = atoi(v);
     if (const char *v = env("FASTKMER_FUSED_PROBE")) c->fused_probe = atoi(v);
@@ -1564,6 +1566,10 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     const bool tiered = pl.tiered;
     const uint32_t cap = pl.cap, wave_cap = pl.wave_cap;
     const uint64_t ncell_all = (uint64_t)c->nlb << F;
+    // useHT=1 (extractKXmersHT, SBKC:664-739): the wave tiers' LDS hash tables emit their keys in
+    // table order (the reference writes its hash map's iteration order, SBKC:723-734), no rank; the
+    // heavier tiers' outputs stay ascending, which is one such order too
+    const bool ordered = !c->cfg.use_ht;
     FK_TRY(ensure(*B.flags, ncell_all * 4));
     FK_TRY(ensure(*B.flag_scan, (ncell_all + 1) * 8));
     FK_TRY(ensure(c->misc, 64));
@@ -1613,11 +1619,11 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
                                                okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                               B.bucket_unique->as<uint64_t>(), nullptr, s));
+                                               B.bucket_unique->as<uint64_t>(), nullptr, s, ordered));
         else
             HIP_TRY(launch_bucket_count128_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
                                                 okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                B.bucket_unique->as<uint64_t>(), s));
+                                                B.bucket_unique->as<uint64_t>(), s, ordered));
         HIP_TRY(hipEventSynchronize(c->tier_ev));
         const uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
         const uint64_t listed_keys = c->pin_tier.as<uint64_t>()[3];
@@ -1659,7 +1665,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                               (unsigned long long)maxsub);
             HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
                                             okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                            c->sp_uniq.as<uint64_t>(), s));
+                                            c->sp_uniq.as<uint64_t>(), s, ordered));
             HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
                                        c->sp_par.as<SplitParent>(), c->sp_subs.as<SubBucket>(),
                                        c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
@@ -1691,7 +1697,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             // the LDS radix sort; buckets above the block tier the streaming path
             HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                     okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                    B.bucket_unique->as<uint64_t>(), ts));
+                                                    B.bucket_unique->as<uint64_t>(), ts, ordered));
             HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), ntier[0], k,
                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                        B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
@@ -2023,11 +2029,11 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
         max_bin = std::max(max_bin, bkm[lb]);
     }
     HIP_TRY(hipEventRecord(c->ev[6], s));
-    if (c->cfg.use_ht && c->cfg.k <= 63)  // k = 64: no spare bit in the hi word (global tables)
+    if (c->cfg.use_ht && c->cfg.k <= 63 && c->ht_groups)
         FK_TRY(reduce_ht_lds(c, chunks, bcb, bkm));
-    else if (c->cfg.use_ht)
+    else if (c->cfg.use_ht && c->cfg.k == 64)  // k = 64: per-bin tables in HBM
         FK_TRY(reduce_ht(c, nchunks, bkm));
-    else
+    else  // the sorted count; useHT=1 with the wave tiers in table order
         FK_TRY(reduce_sorted(c, nchunks, total_kmers, max_bin));
     HIP_TRY(hipEventRecord(c->ev[7], s));
     c->h_bin_off.assign((size_t)nlb + 1, 0);
@@ -2245,10 +2251,10 @@ static void pieces_reset(fk_ctx *c) {
 }
 
 // ---- staged pieces (sorted count, k <= 32): one rank's landed pieces, or the received segments
-// (the hash count and k = 64 count the whole input after the last byte; so do the test hook that
-// routes every bucket through the streaming path and the bucket-kernel probes)
+// (k = 64 counts the whole input after the last byte; so do the test hook that routes every bucket
+// through the streaming path and the bucket-kernel probes)
 static bool staged_ok(const fk_ctx *c) {
-    return !c->cfg.use_ht && c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
+    return !(c->cfg.use_ht && c->ht_groups) && c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
 }
 static bool staged_eligible(const fk_ctx *c) { return staged_ok(c) && c->G == 1 && !c->comm; }
 

@@ -41,6 +41,7 @@ struct RcclApi {
     ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t *, ncclConfig_t *) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -79,6 +80,7 @@ const RcclApi *rccl(std::string &err) {
             SYM(CommInitRank, "ncclCommInitRank");
             SYM(CommDestroy, "ncclCommDestroy");
             SYM(CommAbort, "ncclCommAbort");
+            SYM(CommSplit, "ncclCommSplit");
             SYM(GroupStart, "ncclGroupStart");
             SYM(GroupEnd, "ncclGroupEnd");
             SYM(Send, "ncclSend");
@@ -104,6 +106,12 @@ const RcclApi *rccl(std::string &err) {
     return &g_rccl;
 }
 
+// Two communicators of the same ranks: the records' all-to-all-v on the caller's (comm) stream, and
+// the small host-array collectives (per-step counts, all-reduces) on a communicator split off it
+// (ncclCommSplit) with a stream and staging buffer of their own -- so a step's count exchange does
+// not queue behind the previous step's records still moving on the comm stream (RCCL orders the
+// operations of one communicator across streams).  Every rank issues both kinds in the same order.
+// Without ncclCommSplit both run on the one communicator and the caller's stream.
 class RcclComm : public Comm {
    public:
     RcclComm(const RcclApi *api, ncclComm_t comm, int n, int rank) : api_(api), comm_(comm) {
@@ -112,19 +120,36 @@ class RcclComm : public Comm {
     }
     ~RcclComm() override {
         if (stage_) (void)hipFree(stage_);
+        if (cstream_) {
+            (void)hipStreamSynchronize(cstream_);
+            (void)hipStreamDestroy(cstream_);
+        }
+        if (ccomm_) (void)api_->CommDestroy(ccomm_);
         if (comm_) (void)api_->CommDestroy(comm_);
     }
     const char *kind() const override { return "rccl"; }
 
+    // collective over the ranks (every rank calls it once, right after joining)
+    int init_counts(std::string &err) {
+        if (!api_->CommSplit) return 0;
+        ncclComm_t c2 = nullptr;
+        if (nccl(api_->CommSplit(comm_, 0, rank_, &c2, nullptr), err)) return -1;
+        ccomm_ = c2;
+        COMM_HIP(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking));
+        return 0;
+    }
+
     int alltoall_u64(const uint64_t *in, uint64_t *out, size_t n, hipStream_t s, std::string &err) override {
+        ncclComm_t cm = ccomm_ ? ccomm_ : comm_;
+        if (cstream_) s = cstream_;
         const size_t bytes = (size_t)n_ * n * 8;
         if (stage(2 * bytes, err)) return -1;
         uint64_t *din = static_cast<uint64_t *>(stage_), *dout = din + (size_t)n_ * n;
         COMM_HIP(hipMemcpyAsync(din, in, bytes, hipMemcpyHostToDevice, s));
         if (nccl(api_->GroupStart(), err)) return -1;
         for (int p = 0; p < n_; ++p) {
-            if (nccl(api_->Send(din + (size_t)p * n, n, ncclUint64, p, comm_, s), err)) return end_group(err);
-            if (nccl(api_->Recv(dout + (size_t)p * n, n, ncclUint64, p, comm_, s), err)) return end_group(err);
+            if (nccl(api_->Send(din + (size_t)p * n, n, ncclUint64, p, cm, s), err)) return end_group(err);
+            if (nccl(api_->Recv(dout + (size_t)p * n, n, ncclUint64, p, cm, s), err)) return end_group(err);
         }
         if (nccl(api_->GroupEnd(), err)) return -1;
         COMM_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s));
@@ -134,9 +159,11 @@ class RcclComm : public Comm {
 
     int allreduce_sum_u64(uint64_t *v, size_t n, hipStream_t s, std::string &err) override {
         if (!n) return 0;
+        ncclComm_t cm = ccomm_ ? ccomm_ : comm_;
+        if (cstream_) s = cstream_;
         if (stage(n * 8, err)) return -1;
         COMM_HIP(hipMemcpyAsync(stage_, v, n * 8, hipMemcpyHostToDevice, s));
-        if (nccl(api_->AllReduce(stage_, stage_, n, ncclUint64, ncclSum, comm_, s), err)) return -1;
+        if (nccl(api_->AllReduce(stage_, stage_, n, ncclUint64, ncclSum, cm, s), err)) return -1;
         COMM_HIP(hipMemcpyAsync(v, stage_, n * 8, hipMemcpyDeviceToHost, s));
         COMM_HIP(hipStreamSynchronize(s));
         return 0;
@@ -156,11 +183,16 @@ class RcclComm : public Comm {
     }
 
     void abort() override {
+        if (ccomm_ && api_->CommAbort) {
+            (void)api_->CommAbort(ccomm_);
+            ccomm_ = nullptr;
+        }
         if (comm_ && api_->CommAbort) {
             (void)api_->CommAbort(comm_);
             comm_ = nullptr;
         }
     }
+    bool split_counts() const { return ccomm_ != nullptr; }
 
    private:
     int nccl(ncclResult_t r, std::string &err) {
@@ -185,6 +217,8 @@ class RcclComm : public Comm {
     }
     const RcclApi *api_;
     ncclComm_t comm_;
+    ncclComm_t ccomm_ = nullptr;    // the counts' communicator (split off comm_)
+    hipStream_t cstream_ = nullptr; // ... and its stream
     void *stage_ = nullptr;
     size_t stage_bytes_ = 0;
 };
@@ -379,7 +413,12 @@ Comm *comm_create_rccl(const uint8_t id[COMM_ID_BYTES], int n, int rank, int dev
         return nullptr;
     }
     (void)device;
-    return new RcclComm(a, comm, n, rank);
+    auto *rc = new RcclComm(a, comm, n, rank);
+    if (rc->init_counts(err)) {
+        delete rc;
+        return nullptr;
+    }
+    return rc;
 }
 
 int comm_create_local(int n, const int *devices, Comm **out, std::string &err) {

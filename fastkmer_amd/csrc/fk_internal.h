@@ -194,7 +194,7 @@ constexpr uint32_t WAVE_BUCKET_CAP = 512;
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                                       hipStream_t s);
+                                       hipStream_t s, bool ordered = true);
 hipError_t launch_expand_two_level(int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
                                    uint32_t nlbins, int k, int F, int F2, const uint32_t *sc_pre,
                                    const uint64_t *cell_base, uint64_t *mid, uint64_t *keys, hipStream_t s,
@@ -215,9 +215,10 @@ hipError_t launch_bucket_flags_greedy(const uint64_t *cell_total, uint32_t nlbin
 hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave_cap, uint32_t block_cap,
                                uint64_t *bucket_unique, uint32_t *lists, unsigned int *counts,
                                unsigned long long *listed_keys, hipStream_t s);
+// ordered = false (useHT): every bucket's distinct keys in table order, no rank
 hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
-                                      const uint32_t *list, hipStream_t s);
+                                      const uint32_t *list, hipStream_t s, bool ordered = true);
 // heavy buckets (above the wave tier, k <= 32) split into wave-sized sub-buckets by the key bits
 // below their common prefix (k_bucket_split64), counted by the wave tier (k_sub_count64_wave) and
 // joined back into the bucket's output region (k_bucket_join)
@@ -240,7 +241,7 @@ hipError_t launch_bucket_split64(const BucketSrc &src, const Bucket *buckets, co
                                  SubBucket *subs, SplitParent *parents, unsigned int *counts, uint32_t *fb0,
                                  uint32_t *fb1, uint32_t block_cap, hipStream_t s);
 hipError_t launch_sub_count64_wave(const SubBucket *subs, uint64_t nsubs, const uint64_t *skeys, uint64_t *out_keys,
-                                   uint32_t *out_counts, uint64_t *sub_unique, hipStream_t s);
+                                   uint32_t *out_counts, uint64_t *sub_unique, hipStream_t s, bool ordered = true);
 hipError_t launch_bucket_join(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
                               uint32_t n1, const SplitParent *parents, const SubBucket *subs,
                               const uint64_t *sub_unique, uint64_t *out_keys, uint32_t *out_counts,
@@ -257,7 +258,7 @@ hipError_t launch_bucket_sort(int KW, const BucketSrc &src, const Bucket *bucket
 constexpr uint32_t WAVE128_MID_CAP = 512;
 hipError_t launch_bucket_count128_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
                                            uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
-                                           uint64_t *bucket_unique, hipStream_t s);
+                                           uint64_t *bucket_unique, hipStream_t s, bool ordered = true);
 hipError_t launch_bucket_sort_large(int KW, const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                     uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
                                     uint64_t *bucket_unique, const uint32_t *list, hipStream_t s);

@@ -8,8 +8,8 @@ A bin's multiset is the sum of its pieces' multisets, so the result must be
 bit-exact against the CPU oracle over the whole input -- checked here at sizes
 the oracle finishes quickly, with the pieces made small (FASTKMER_PIECE_BYTES)
 so that inputs of a few MB cross several of them, for key distributions that
-differ from piece to piece.  The hash count and k = 64 count the whole input
-after the last byte.
+differ from piece to piece.  useHT=1 stages the same way (its buckets are
+counted in table order); k = 64 counts the whole input after the last byte.
 """
 import numpy as np
 import pytest
@@ -98,12 +98,13 @@ def test_piece_counts_fallback_counts_whole_input(small_pieces):
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
 
 
-def test_piece_counts_hash_mode_counts_once(small_pieces):
-    # useHT=1: the whole input is counted in fk_finish
-    fasta = fk.synth_fasta(20_000, 100, 400_000, seed=0xA5)
-    kc = count_pinned(fasta, 28, 10, use_ht=True)
-    assert kc.stats()["pieces_counted"] == 0
-    assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048), ordered=False)
+@pytest.mark.parametrize("k,m,read_len", [(28, 10, 100), (55, 12, 150)])
+def test_piece_counts_hash_mode_staged(small_pieces, k, m, read_len):
+    # useHT=1 stages its pieces like the sorted count; the wave tiers emit table order
+    fasta = fk.synth_fasta(20_000, read_len, 400_000, seed=0xA5 + k)
+    kc = count_pinned(fasta, k, m, use_ht=True)
+    assert kc.stats()["pieces_counted"] == 4
+    assert_same_as_oracle(kc, oracle.OracleResult(fasta, k, m, 2048), ordered=False)
 
 
 def test_piece_counts_many_small_pieces(monkeypatch):
