@@ -58,7 +58,7 @@ class fk_stats(ctypes.Structure):
                                        ("xch_bytes_received", ctypes.c_uint64), ("ms_exchange", ctypes.c_double),
                                        ("ms_exchange_tail", ctypes.c_double),
                                        ("pieces_counted", ctypes.c_uint64), ("ms_merge", ctypes.c_double),
-                                       ("precounted", ctypes.c_uint64), ("block_buckets", ctypes.c_uint64), ("big_buckets", ctypes.c_uint64),
+                                       ("heavy_keys", ctypes.c_uint64), ("block_buckets", ctypes.c_uint64), ("big_buckets", ctypes.c_uint64),
                                        ("ht_big_groups", ctypes.c_uint64), ("split_buckets", ctypes.c_uint64),
                                        ("sub_buckets", ctypes.c_uint64)]
 

@@ -107,7 +107,7 @@ def _build_lib(lib: str, deps: list[str], force: bool, defs: list[str]) -> None:
 
 def build_probes(force: bool = False) -> str:
     """A measurement-only library with the result-altering timing probes compiled in (-DFK_PROBES:
-    FASTKMER_FUSED_PROBE, FASTKMER_DEBUG_PHASE, FASTKMER_LH_PROBE, FASTKMER_SPLIT_MAP, the host trace
+    FASTKMER_FUSED_PROBE, FASTKMER_DEBUG_PHASE, FASTKMER_SPLIT_MAP, the host trace
     FASTKMER_HOST_TRACE and the map phase stamps).
     Scripts select it with FASTKMER_LIB; nothing else loads it."""
     deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "fastkmer.h")]

@@ -14,6 +14,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <unordered_map>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -98,7 +99,9 @@ int ensure(DevBuf &b, size_t bytes) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
-    const size_t want = bytes + bytes / 8 + 256;
+    // slack for the next job's slightly larger input: an eighth, at most 1 GiB (4 GB of slack on each
+    // k-mer array of a 6.25 GB job would cost more HBM than the reallocations it saves)
+    const size_t want = bytes + std::min<size_t>(bytes / 8, 1ull << 30) + 256;
     hipError_t e = hipMalloc(&b.p, want);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -301,13 +304,6 @@ struct fk_ctx {
     DevBuf rec_code;              // fused map: per tile, the tile's 2-bit code stream (map_fused_cslot() words)
     DevBuf tstat;                 // fused map: per tile (k-mers, positions)
     DevBuf map_vslots;            // split map: the parse kernel's valid streams for the passes (MAP_VSLOT_TILES tiles)
-    // hash count in LDS tables (fk_count_lds.inc)
-    DevBuf lh_meta, lh_H, lh_off, lh_groups, lh_items, lh_recs, lh_spill[2], lh_sp[2], lh_okeys, lh_ocnt;
-    DevBuf lh_parents, lh_parents2, lh_plan, lh_suboff, lh_part, lh_glist;  // spill rounds: parents, their plan, sub-ranges
-    double lh_ratio = 0.25;       // distinct / k-mers of the last hash count (sizes the next one's groups)
-    uint32_t lh_big_thr = 1800;   // FASTKMER_HT_BIG (test hook): k > 32, groups of more k-mers take 6144-slot tables
-    int ht_groups = 0;            // FASTKMER_HT_GROUPS=1: useHT on the (bin, signature hash) group tables (A/B)
-    int lh_probe = 0;             // FASTKMER_LH_PROBE (-DFK_PROBES): stop the combine kernel after a phase
     bool rec_tiled = false;       // records: the fused map's tiles (else dense, c->nrec)
     uint64_t rec_tiles = 0;       // tiles of the tiled layout
     uint64_t nrec = 0, nkmers = 0;
@@ -322,7 +318,6 @@ struct fk_ctx {
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_total;
-    DevBuf table_off, tkeys, tstate, tcounts;
     DevBuf sp_base, sp_keys, sp_subs, sp_par, sp_uniq, sp_fb;  // heavy buckets split into sub-buckets
     ScanWorkspace ws;
     // results
@@ -337,7 +332,6 @@ struct fk_ctx {
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
     PinBuf pin_up, pin_down;              // staging: chunk tables up, per-bin counts down
     PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
-    PinBuf pin_ht;                        // hash count: spilled parents down, spill-round items up
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
     bool distinct_pending = false;        // the sorted count's distinct total arrives with the bin offsets
@@ -346,10 +340,6 @@ struct fk_ctx {
     // bin-ordered result, bin_off / h_bin_off per bin.  Readers gather a bin's buckets (fk_get_bin) or
     // the whole result (fk_write_bins).
     bool gapped = false, dense_ready = false;
-    // The LDS hash count's result stays in the bins' regions: local bin lb's distinct entries at
-    // h_ht_kbase[lb] of lh_okeys / lh_ocnt (no packing pass; fk_write_bins packs it once).
-    bool ht_regions = false;
-    std::vector<uint64_t> h_ht_kbase;
     const uint64_t *res_keys = nullptr;   // okb of the last sorted count (out_keys, or mid)
     const uint64_t *res_fs = nullptr;     // flag_scan of its bucket cut
     uint64_t res_nbuckets = 0;
@@ -540,13 +530,10 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *v = env("FASTKMER_DEBUG_CELL_TARGET")) c->cell_target = (uint32_t)atoi(v);
     if (const char *v = env("FASTKMER_X2_L1")) c->x2_l1 = atoi(v);
     if (const char *v = env("FASTKMER_FUSED")) c->fused = atoi(v);
-    if (const char *v = env("FASTKMER_HT_BIG")) c->lh_big_thr = (uint32_t)strtoul(v, nullptr, 10);
-    if (const char *v = env("FASTKMER_HT_GROUPS")) c->ht_groups = atoi(v);
 #ifdef FK_PROBES
     if (const char *v = env("FASTKMER_DEBUG_PHASE")) c->dbg_phase = atoi(v);
     if (const char *v = env("FASTKMER_FUSED_PROBE")) c->fused_probe = atoi(v);
     if (const char *v = env("FASTKMER_SPLIT_MAP")) c->split_map = atoi(v);
-    if (const char *v = env("FASTKMER_LH_PROBE")) c->lh_probe = atoi(v);
 #endif
     if (cfg->device >= 0) {
         if (cfg->device >= ndev) {
@@ -609,14 +596,11 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat, &c->map_vslots,
-                      &c->lh_meta, &c->lh_H, &c->lh_off, &c->lh_groups, &c->lh_items, &c->lh_recs, &c->lh_spill[0],
-                      &c->lh_spill[1], &c->lh_sp[0], &c->lh_sp[1], &c->lh_okeys, &c->lh_ocnt, &c->lh_parents, &c->lh_parents2, &c->lh_plan, &c->lh_suboff, &c->lh_part, &c->lh_glist,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
                       &c->chunk_base, &c->lp, &c->scratch,
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
-                      &c->dense_counts, &c->bin_off, &c->misc, &c->table_off, &c->tkeys, &c->tstate,
-                      &c->tcounts, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts,
+                      &c->dense_counts, &c->bin_off, &c->misc, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts,
                       &c->sp_base, &c->sp_keys, &c->sp_subs, &c->sp_par, &c->sp_uniq, &c->sp_fb};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
@@ -629,7 +613,6 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->pin_up.release();
     c->pin_down.release();
     c->pin_tier.release();
-    c->pin_ht.release();
     c->file_pin[0].release();
     c->file_pin[1].release();
     if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
@@ -680,7 +663,7 @@ FK_EXPORT int32_t fk_num_bins(const fk_ctx *c) { return c ? c->Bc : 0; }
 static void reset_results(fk_ctx *c) {
     c->mapped = false;
     c->have_result = false;
-    c->gapped = c->dense_ready = c->ht_regions = false;
+    c->gapped = c->dense_ready = false;
     c->distinct = 0;
     c->h_bin_off.clear();
 }
@@ -769,6 +752,7 @@ static void pieces_reset(fk_ctx *c);
 // source has been read (the caller's buffer is free); the map of the last
 // segment may still be running.
 static int comm_fail(fk_ctx *c, int rc);
+static int note_held(fk_ctx *c, int rc);
 
 static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     if (!fasta && n) return set_err(FK_E_INVALID, "null argument");
@@ -899,7 +883,7 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
 FK_EXPORT int fk_ingest(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     const int rc = ingest_impl(c, fasta, n, last);
-    return rc && c->comm ? comm_fail(c, rc) : rc;
+    return rc && c->comm ? comm_fail(c, rc) : note_held(c, rc);
 }
 
 static int reserve_impl(fk_ctx *c, uint64_t total_bytes);
@@ -1603,6 +1587,8 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
     c->stats.buckets = nbuckets;
     c->stats.fine_bits = (uint64_t)F;
+    c->stats.heavy_keys = 0;
+    c->stats.split_buckets = c->stats.sub_buckets = 0;
     if (tiered) {
         FK_TRY(ensure(*B.tier_list, nbuckets * 8));
         uint32_t *lists = B.tier_list->as<uint32_t>();
@@ -1627,6 +1613,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         HIP_TRY(hipEventSynchronize(c->tier_ev));
         const uint32_t ntier[2] = {c->pin_tier.as<uint32_t>()[0], c->pin_tier.as<uint32_t>()[1]};
         const uint64_t listed_keys = c->pin_tier.as<uint64_t>()[3];
+        c->stats.heavy_keys = listed_keys;
         htrace("sorted: tiers read");
         c->stats.block_buckets = ntier[0];
         c->stats.big_buckets = ntier[1];
@@ -1654,13 +1641,43 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
                                           c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
                                           c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb, fb + nl,
-                                          cap, s));
+                                          cap, k, F, s));
             HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(c->tier_ev, s));
             HIP_TRY(hipEventSynchronize(c->tier_ev));
             const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
             const uint32_t nsub = sc[0], nfb0 = sc[1], nfb1 = sc[2];
             htrace("sorted: split counts read");
+#ifdef FK_PROBES
+            if (getenv("FASTKMER_HOST_TRACE")) {  // the listed buckets by size class: buckets, keys, fallbacks
+                std::vector<uint64_t> base((size_t)nl + 1);
+                std::vector<uint32_t> f(2 * (size_t)nl);
+                HIP_TRY(hipMemcpy(base.data(), c->sp_base.p, base.size() * 8, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(f.data(), fb, f.size() * 4, hipMemcpyDeviceToHost));
+                std::vector<uint32_t> h_l((size_t)nl);
+                HIP_TRY(hipMemcpy(h_l.data(), lists, (size_t)ntier[0] * 4, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(h_l.data() + ntier[0], l1, (size_t)ntier[1] * 4, hipMemcpyDeviceToHost));
+                std::unordered_map<uint32_t, uint32_t> pos;
+                for (uint32_t j = 0; j < nl; ++j) pos[h_l[j]] = j;
+                uint64_t hb[40] = {}, hk[40] = {}, hf[40] = {}, hfk[40] = {};
+                std::vector<char> isfb(nl, 0);
+                for (uint32_t j = 0; j < nfb0; ++j) isfb[pos[f[j]]] = 1;
+                for (uint32_t j = 0; j < nfb1; ++j) isfb[pos[f[nl + j]]] = 1;
+                for (uint32_t j = 0; j < nl; ++j) {
+                    const uint64_t n = base[j + 1] - base[j];
+                    const int cl = 63 - __builtin_clzll(n | 1);
+                    hb[cl] += 1, hk[cl] += n;
+                    if (isfb[j]) hf[cl] += 1, hfk[cl] += n;
+                }
+                fprintf(stderr, "probe_split: listed %u keys %llu subs %u fallbacks %u + %u\n", nl,
+                        (unsigned long long)base[nl], nsub, nfb0, nfb1);
+                for (int cl = 0; cl < 40; ++cl)
+                    if (hb[cl])
+                        fprintf(stderr, "probe_split: n in [2^%d, 2^%d): buckets %llu keys %llu fallback buckets %llu keys %llu\n",
+                                cl, cl + 1, (unsigned long long)hb[cl], (unsigned long long)hk[cl],
+                                (unsigned long long)hf[cl], (unsigned long long)hfk[cl]);
+            }
+#endif
             if (nsub > maxsub) return set_err(FK_E_DEVICE, "bucket split: %u sub-buckets of at most %llu", nsub,
                                               (unsigned long long)maxsub);
             HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
@@ -1763,10 +1780,11 @@ static int sorted_result(fk_ctx *c, int F, uint64_t nbuckets, DevBuf &okb, Count
 }
 
 static int sorted_count(fk_ctx *c, const SortedPlan &pl, const BucketSrc &src_in, uint64_t total_kmers) {
-    // the one-array count writes its buckets' results over the first expansion level (`mid` is dead
-    // once level 2 has run, stream order): one k-mer array less on the device (57 GB at configs[3]'s
-    // per-GPU load, 128-bit keys)
-    DevBuf &okb = (src_in.np == 0 && pl.two_level && c->mid.bytes >= total_kmers * 8 * c->KW) ? c->mid : c->out_keys;
+    // the two-level count writes its buckets' results over the first expansion level (`mid` is dead
+    // once level 2 has run, stream order; a staged job's `mid` held one piece and grows to the job
+    // here, its contents dead): one k-mer array less on the device (57 GB at configs[3]'s per-GPU
+    // load, 128-bit keys; 36 GB at configs[2]'s)
+    DevBuf &okb = pl.two_level ? c->mid : c->out_keys;
     uint64_t nb = 0;
     FK_TRY(sorted_count_buckets(c, pl, src_in, total_kmers, c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(),
                                 main_bufs(c), okb, &nb));
@@ -1784,215 +1802,6 @@ static int reduce_sorted(fk_ctx *c, uint32_t nchunks, uint64_t total_kmers, uint
     FK_TRY(sorted_expand(c, pl, nchunks, total_kmers, c->keys, c->cell_base));
     BucketSrc src{c->keys.as<uint64_t>(), pl.F};
     return sorted_count(c, pl, src, total_kmers);
-}
-
-// Hash count in LDS tables (fk_count_lds.inc): bins split into 2^f_b groups by
-// the records' signature fine hash, one workgroup per group, spill rounds until
-// every key is counted, then the bins' regions packed densely.  f_b is sized so
-// a group's expected distinct k-mers (k-mers x the last run's distinct ratio)
-// fill about half a table.
-static int reduce_ht_lds(fk_ctx *c, const std::vector<Chunk> &chunks, const std::vector<uint32_t> &bcb,
-                         const std::vector<uint64_t> &bin_kmers) {
-    hipStream_t s = c->stream;
-    const uint32_t nlb = c->nlb, nchunks = (uint32_t)chunks.size();
-    const uint32_t KW = (uint32_t)c->KW;
-    // LH_TS / LH2_TS slots, half full (0.35 / 0.25 of a table measured slower at configs[1] and the
-    // configs[2] shape, profiles/r04c_ht_load_ab.txt)
-    const double per_group = (KW == 1 ? 4096.0 : 2048.0) * 0.5;
-    std::vector<uint8_t> flog(nlb, 0);
-    std::vector<uint32_t> gbase(nlb + 1, 0);
-    std::vector<uint64_t> rec_base(nlb + 1, 0), km_base(nlb + 1, 0);
-    for (uint32_t lb = 0; lb < nlb; ++lb) {
-        const double want = (double)bin_kmers[lb] * c->lh_ratio / per_group;
-        int f = 0;
-        while (f < LH_MAX_FLOG && (double)(1u << f) < want) ++f;
-        flog[lb] = (uint8_t)f;
-        gbase[lb + 1] = gbase[lb] + (1u << f);
-        uint64_t nr = 0;
-        for (uint32_t ch = bcb[lb]; ch < bcb[lb + 1]; ++ch) nr += chunks[ch].rec_end - chunks[ch].rec_begin;
-        rec_base[lb + 1] = rec_base[lb] + nr;
-        km_base[lb + 1] = km_base[lb] + bin_kmers[lb];
-    }
-    const uint32_t ngroups = gbase[nlb];
-    const uint64_t nrec = rec_base[nlb], nkm = km_base[nlb];
-    // one upload: rec_base, km_base (u64), gbase (u32), flog (u8)
-    const size_t meta_bytes = (size_t)(nlb + 1) * 16 + (size_t)(nlb + 1) * 4 + nlb + 16;
-    std::vector<uint8_t> meta(meta_bytes);
-    std::memcpy(meta.data(), rec_base.data(), (nlb + 1) * 8);
-    std::memcpy(meta.data() + (nlb + 1) * 8, km_base.data(), (nlb + 1) * 8);
-    std::memcpy(meta.data() + (nlb + 1) * 16, gbase.data(), (nlb + 1) * 4);
-    std::memcpy(meta.data() + (nlb + 1) * 20, flog.data(), nlb);
-    FK_TRY(ensure(c->lh_meta, meta_bytes));
-    HIP_TRY(hipMemcpyAsync(c->lh_meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, s));
-    const uint64_t *d_rec_base = c->lh_meta.as<uint64_t>(), *d_km_base = d_rec_base + (nlb + 1);
-    const uint32_t *d_gbase = reinterpret_cast<const uint32_t *>(d_rec_base + 2 * (uint64_t)(nlb + 1));
-    const uint8_t *d_flog = reinterpret_cast<const uint8_t *>(d_gbase + (nlb + 1));
-    FK_TRY(ensure(c->lh_H, (uint64_t)nchunks * 64 * 8 + 64));
-    FK_TRY(ensure(c->lh_off, (uint64_t)nchunks * 64 * 8 + 64));
-    FK_TRY(ensure(c->lh_groups, (uint64_t)ngroups * sizeof(LhGroup) + 64));
-    FK_TRY(ensure(c->lh_recs, nrec * c->W * 8 + 64));
-    FK_TRY(ensure(c->lh_spill[0], nkm * 8 * KW + 64));
-    FK_TRY(ensure(c->lh_okeys, nkm * 8 * KW + 64));
-    FK_TRY(ensure(c->lh_ocnt, nkm * 4 + 64));
-    FK_TRY(ensure(c->misc, 64));
-    FK_TRY(ensure(c->bin_off, ((uint64_t)nlb + 1) * 8));
-    FK_TRY(ensure(c->table_off, ((uint64_t)nlb + 1) * 8));  // per-bin distinct counts
-    uint32_t *Hr = c->lh_H.as<uint32_t>(), *Hk = Hr + (uint64_t)nchunks * 64;
-    LhGroup *groups = c->lh_groups.as<LhGroup>();
-    HIP_TRY(launch_fine_partition(c->W, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->bin_chunk_begin.as<uint32_t>(),
-                                  nlb, d_flog, d_rec_base, d_km_base, d_gbase, Hr, Hk, c->lh_off.as<uint64_t>(),
-                                  groups, c->lh_recs.as<uint64_t>(), s));
-    unsigned long long *bin_cnt = c->table_off.as<unsigned long long>();
-    unsigned long long *sp_total = c->misc.as<unsigned long long>();  // [0] keys spilled, [1] spilled groups
-    HIP_TRY(hipMemsetAsync(bin_cnt, 0, ((uint64_t)nlb + 1) * 8, s));
-    HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
-    FK_TRY(ensure(c->lh_sp[0], (uint64_t)ngroups * 4 + 64));
-    if (c->pin_ht.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-    uint64_t *const pin = c->pin_ht.as<uint64_t>();
-    // 128-bit keys: the groups of more than lh_big_thr k-mers take 6144-slot tables (one 1024-thread
-    // workgroup per CU) instead of spilling most of their keys from the 2048-slot ones.  (A 3072-slot
-    // tier between them and 8192-slot tables for 64-bit keys measured slower, profiles/r04c_ht4_mid_
-    // tier_probes.txt, r04c_ht5_big64.txt: at k = 28 over a 3 Gbp genome every group overflows.)
-    uint64_t nbig = 0;
-    const uint32_t big_thr = KW == 2 ? c->lh_big_thr : 0u;
-    if (big_thr) {
-        FK_TRY(ensure(c->lh_glist, (uint64_t)ngroups * 4 + 64));
-        HIP_TRY(launch_ht_big_list(groups, ngroups, big_thr, 0u, c->lh_glist.as<uint32_t>(), sp_total + 1, s));
-        HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        nbig = pin[1];
-    }
-    c->stats.ht_big_groups = nbig;
-    HIP_TRY(launch_ht_combine(c->W, c->lh_recs.as<uint64_t>(), groups, nullptr, ngroups, c->cfg.k, 0,
-                              c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total, d_km_base, bin_cnt,
-                              c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s, c->lh_probe, nullptr, nullptr,
-                              nbig ? big_thr : 0u));
-    if (nbig)
-        HIP_TRY(launch_ht_combine128_big(c->lh_recs.as<uint64_t>(), groups, c->lh_glist.as<uint32_t>(), (uint32_t)nbig,
-                                         c->cfg.k, c->lh_spill[0].as<uint64_t>(), c->lh_sp[0].as<uint32_t>(), sp_total,
-                                         d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(), c->lh_ocnt.as<uint32_t>(), s));
-    // the groups that spilled, listed on the device (a parent each: its spill range and count)
-    FK_TRY(ensure(c->lh_parents, (uint64_t)ngroups * sizeof(LhItem) + 64));
-    HIP_TRY(launch_ht_spill_list(groups, c->lh_sp[0].as<uint32_t>(), ngroups, c->lh_parents.as<LhItem>(),
-                                 sp_total + 1, s));
-    HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    uint64_t spilled = pin[0], np = pin[1];
-    c->stats.ht_spilled = spilled;
-    // spill rounds, planned on the device (the host reads three totals per round): each spilled
-    // range (a parent) is split by a salted key hash into 2^slog sub-items of about per_group keys,
-    // so one heavy signature (a group far beyond a table) takes one more round instead of one per
-    // table's worth of keys.  The sub-items of a parent partition its keys, so they share one
-    // spill range of the parent's size (a cursor per parent): a round's spill space is at most the
-    // previous round's spilled keys.  Parents of 2..2^LH_SUB_MAXLOG sub-items are first
-    // partitioned by sub-item (k_ht_subpart), so a sub-item reads its own keys only.  A round's
-    // parents are at most the previous round's (one spill range each).
-    if (spilled) FK_TRY(ensure(c->lh_parents2, np * sizeof(LhItem) + 64));
-    LhItem *par = c->lh_parents.as<LhItem>(), *par_next = c->lh_parents2.as<LhItem>();
-    int cur = 0, rounds = 1;
-    while (spilled) {
-        if (++rounds > 16) return set_err(FK_E_DEVICE, "hash count: spill rounds do not converge");
-        const int nxt = cur ^ 1;
-        FK_TRY(ensure(c->lh_plan, (6 * np + 4) * 8));
-        uint64_t *const pl = c->lh_plan.as<uint64_t>();
-        uint64_t *const cnt = pl, *const nsub = pl + np, *const npad = pl + 2 * np, *const region = pl + 3 * np,
-                       *const item_off = pl + 4 * np, *const pad_off = pl + 5 * np, *const tot = pl + 6 * np;
-        HIP_TRY(launch_ht_plan(par, (uint32_t)np, per_group, 1, cnt, nsub, npad, s));
-        HIP_TRY(scan_excl_sum_u64(cnt, region, np, tot, c->ws, s));
-        HIP_TRY(scan_excl_sum_u64(nsub, item_off, np, tot + 1, c->ws, s));
-        HIP_TRY(scan_excl_sum_u64(npad, pad_off, np, tot + 2, c->ws, s));
-        HIP_TRY(hipMemcpyAsync(pin, tot, 24, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        const uint64_t out = pin[0], ni = pin[1], nsub_off = pin[2];
-        if (ni > 0xffffffffull) return set_err(FK_E_DEVICE, "hash count: %llu spill items", (unsigned long long)ni);
-        FK_TRY(ensure(c->lh_items, ni * sizeof(LhItem) + 64));
-        FK_TRY(ensure(c->lh_suboff, nsub_off * 4 + 64));
-        if (nsub_off) FK_TRY(ensure(c->lh_part, c->lh_spill[cur].bytes));
-        FK_TRY(ensure(c->lh_spill[nxt], out * 8 * KW + 64));
-        FK_TRY(ensure(c->lh_sp[nxt], np * 4 + 64));
-        LhItem *d_items = c->lh_items.as<LhItem>();
-        HIP_TRY(launch_ht_items(par, (uint32_t)np, region, item_off, pad_off, npad, d_items, s));
-        if (nsub_off)
-            HIP_TRY(launch_ht_subpart((int)KW, c->lh_spill[cur].as<uint64_t>(), par, (uint32_t)np, (uint32_t)rounds,
-                                      c->lh_part.as<uint64_t>(), c->lh_suboff.as<uint32_t>(), s));
-        HIP_TRY(hipMemsetAsync(c->lh_sp[nxt].p, 0, np * 4, s));
-        HIP_TRY(hipMemsetAsync(sp_total, 0, 16, s));
-        HIP_TRY(launch_ht_combine(c->W, c->lh_spill[cur].as<uint64_t>(), groups, d_items, (uint32_t)ni, c->cfg.k,
-                                  (uint32_t)rounds, c->lh_spill[nxt].as<uint64_t>(), c->lh_sp[nxt].as<uint32_t>(),
-                                  sp_total, d_km_base, bin_cnt, c->lh_okeys.as<uint64_t>(),
-                                  c->lh_ocnt.as<uint32_t>(), s, 0, c->lh_part.as<uint64_t>(),
-                                  c->lh_suboff.as<uint32_t>()));
-        HIP_TRY(launch_ht_next_parents(par, (uint32_t)np, region, c->lh_sp[nxt].as<uint32_t>(), par_next, sp_total + 1,
-                                       s));
-        HIP_TRY(hipMemcpyAsync(pin, sp_total, 16, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        spilled = pin[0];
-        np = pin[1];
-        c->stats.ht_spilled += spilled;
-        std::swap(par, par_next);
-        cur = nxt;
-    }
-    c->stats.ht_rounds = (uint64_t)rounds;
-    // dense output: bin_off = scan of the per-bin distinct counts
-    HIP_TRY(scan_excl_sum_u64(reinterpret_cast<const uint64_t *>(bin_cnt), c->bin_off.as<uint64_t>(), nlb,
-                              c->bin_off.as<uint64_t>() + nlb, c->ws, s));
-    uint64_t distinct = 0;
-    HIP_TRY(hipMemcpyAsync(&distinct, c->bin_off.as<uint64_t>() + nlb, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    // the result stays in the bins' regions (measured: packing it densely cost 17.9 ms of a 67 ms
-    // count at the configs[3] shape); materialize_dense packs it for fk_write_bins
-    c->ht_regions = true;
-    c->dense_ready = false;
-    c->h_ht_kbase = km_base;
-    c->distinct = distinct;
-    if (nkm) c->lh_ratio = std::min(1.0, std::max(0.02, (double)distinct / (double)nkm));
-    return FK_OK;
-}
-
-static int reduce_ht(fk_ctx *c, uint32_t nchunks, const std::vector<uint64_t> &bin_kmers) {
-    hipStream_t s = c->stream;
-    std::vector<uint64_t> toff(c->nlb + 1, 0);
-    for (uint32_t lb = 0; lb < c->nlb; ++lb) {
-        uint64_t cap = 16;
-        while (cap < 2 * bin_kmers[lb]) cap <<= 1;  // load factor <= 1/2 (upper bound of distinct)
-        toff[lb + 1] = toff[lb] + (bin_kmers[lb] ? cap : 0);
-    }
-    const uint64_t nslots = toff[c->nlb];
-    FK_TRY(ensure(c->table_off, ((uint64_t)c->nlb + 1) * 8));
-    FK_TRY(ensure(c->tkeys, nslots * 8 * c->KW));
-    FK_TRY(ensure(c->tcounts, nslots * 4));
-    FK_TRY(ensure(c->tstate, c->KW == 2 ? nslots * 4 : 16));
-    FK_TRY(ensure(c->flags, nslots * 4));
-    FK_TRY(ensure(c->flag_scan, (nslots + 1) * 8));
-    FK_TRY(ensure(c->misc, 64));
-    FK_TRY(ensure(c->bin_off, ((uint64_t)c->nlb + 1) * 8));
-    HIP_TRY(hipMemcpyAsync(c->table_off.p, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(c->tkeys.p, 0xff, nslots * 8 * c->KW, s));
-    HIP_TRY(hipMemsetAsync(c->tcounts.p, 0, nslots * 4, s));
-    if (c->KW == 2) HIP_TRY(hipMemsetAsync(c->tstate.p, 0, nslots * 4, s));
-    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
-    HIP_TRY(launch_ht_insert(c->W, c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->cfg.k,
-                             c->table_off.as<uint64_t>(), c->tkeys.as<uint64_t>(), c->tstate.as<uint32_t>(),
-                             c->tcounts.as<uint32_t>(), c->misc.as<unsigned long long>(), s));
-    HIP_TRY(launch_ht_flags(c->tcounts.as<uint32_t>(), nslots, c->flags.as<uint32_t>(), s));
-    HIP_TRY(scan_excl_sum_u32_to_u64(c->flags.as<uint32_t>(), c->flag_scan.as<uint64_t>(), nslots,
-                                     c->flag_scan.as<uint64_t>() + nslots, c->ws, s));
-    uint64_t h[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(&h[0], c->flag_scan.as<uint64_t>() + nslots, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&h[1], c->misc.p, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (h[1]) return set_err(FK_E_DEVICE, "hash table overflow (%llu inserts failed)", (unsigned long long)h[1]);
-    const uint64_t distinct = h[0];
-    FK_TRY(ensure(c->dense_keys, distinct * 8 * c->KW));
-    FK_TRY(ensure(c->dense_counts, distinct * 4));
-    HIP_TRY(launch_ht_compact(c->KW, c->tkeys.as<uint64_t>(), c->tcounts.as<uint32_t>(), nslots,
-                              c->flag_scan.as<uint64_t>(), c->dense_keys.as<uint64_t>(),
-                              c->dense_counts.as<uint32_t>(), s));
-    HIP_TRY(launch_ht_bin_offsets(c->flag_scan.as<uint64_t>(), c->table_off.as<uint64_t>(), c->nlb, distinct,
-                                  c->bin_off.as<uint64_t>(), s));
-    c->distinct = distinct;
-    return FK_OK;
 }
 
 // Chunks of <= CHUNK_RECORDS records per local bin (chunks never span bins;
@@ -2029,12 +1838,8 @@ static int reduce_tail(fk_ctx *c, uint64_t nrecv, const std::vector<Chunk> &chun
         max_bin = std::max(max_bin, bkm[lb]);
     }
     HIP_TRY(hipEventRecord(c->ev[6], s));
-    if (c->cfg.use_ht && c->cfg.k <= 63 && c->ht_groups)
-        FK_TRY(reduce_ht_lds(c, chunks, bcb, bkm));
-    else if (c->cfg.use_ht && c->cfg.k == 64)  // k = 64: per-bin tables in HBM
-        FK_TRY(reduce_ht(c, nchunks, bkm));
-    else  // the sorted count; useHT=1 with the wave tiers in table order
-        FK_TRY(reduce_sorted(c, nchunks, total_kmers, max_bin));
+    // the sorted count; useHT=1 (extractKXmersHT) the same with the wave tiers in table order
+    FK_TRY(reduce_sorted(c, nchunks, total_kmers, max_bin));
     HIP_TRY(hipEventRecord(c->ev[7], s));
     c->h_bin_off.assign((size_t)nlb + 1, 0);
     if (c->pin_down.ensure(((size_t)nlb + 1) * 8)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
@@ -2254,7 +2059,7 @@ static void pieces_reset(fk_ctx *c) {
 // (k = 64 counts the whole input after the last byte; so do the test hook that routes every bucket
 // through the streaming path and the bucket-kernel probes)
 static bool staged_ok(const fk_ctx *c) {
-    return !(c->cfg.use_ht && c->ht_groups) && c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
+    return c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
 }
 static bool staged_eligible(const fk_ctx *c) { return staged_ok(c) && c->G == 1 && !c->comm; }
 
@@ -2340,7 +2145,6 @@ static int staged_count(fk_ctx *c) {
     }
     c->stats.ms_partition = mp;
     c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]);
-    c->stats.precounted = 0;
     c->stats.ms_merge = 0.0;
     c->stats.pieces_counted = c->st_np;
     c->stats.records_received = c->nrec;
@@ -2437,7 +2241,36 @@ static void xch_reset(fk_ctx *c) {
     c->xch = fk_ctx::Xch{};
 }
 
+// FK_E_NOMEM from an exported call: the message names what the context holds on the device, largest
+// first, so an oversized job shows which of its arrays to size (or free) without a re-run.
+static int note_held(fk_ctx *c, int rc) {
+    if (rc != FK_E_NOMEM || !c) return rc;
+    std::vector<std::pair<size_t, std::string>> v;
+    auto add = [&](const char *name, const DevBuf &b) {
+        if (b.bytes >= (64u << 20)) v.emplace_back(b.bytes, name);
+    };
+#define FK_HELD(b) add(#b, c->b)
+    FK_HELD(fasta_own); FK_HELD(rec_hdr); FK_HELD(rec_pos); FK_HELD(rec_code); FK_HELD(records);
+    FK_HELD(codes); FK_HELD(valid); FK_HELD(precs); FK_HELD(chunks); FK_HELD(lp); FK_HELD(mid);
+    FK_HELD(scratch); FK_HELD(keys); FK_HELD(out_keys); FK_HELD(out_counts); FK_HELD(buckets);
+    FK_HELD(flags); FK_HELD(flag_scan); FK_HELD(cell_total); FK_HELD(cell_base); FK_HELD(dense_keys);
+    FK_HELD(dense_counts); FK_HELD(bucket_unique);
+    FK_HELD(sp_keys); FK_HELD(sp_subs); FK_HELD(sp_uniq); FK_HELD(xsend); FK_HELD(xrecv);
+    FK_HELD(gather_keys); FK_HELD(st_keys[0]); FK_HELD(st_keys[1]); FK_HELD(st_keys[2]); FK_HELD(st_keys[3]);
+    FK_HELD(part.K); FK_HELD(part.KT); FK_HELD(dest.K); FK_HELD(dest.KT);
+#undef FK_HELD
+    std::sort(v.rbegin(), v.rend());
+    size_t total = 0;
+    for (const auto &e : v) total += e.first;
+    std::string msg = g_err + "; held on the device: " + std::to_string(total >> 20) + " MiB in";
+    for (size_t i = 0; i < v.size() && i < 12; ++i)
+        msg += (i ? ", " : " ") + v[i].second + " " + std::to_string(v[i].first >> 20) + " MiB";
+    g_err = msg;
+    return rc;
+}
+
 static int comm_fail(fk_ctx *c, int rc) {
+    note_held(c, rc);
     if (c->comm) c->comm->abort();  // peers blocked in a step return instead of waiting
     return rc;
 }
@@ -2710,6 +2543,8 @@ static int finish_exchange(fk_ctx *c) {
     return FK_OK;
 }
 
+static int finish_local(fk_ctx *c);
+
 FK_EXPORT int fk_finish(fk_ctx *c) {
     htrace("fk_finish: enter");
     if (!c) return set_err(FK_E_INVALID, "null ctx");
@@ -2718,6 +2553,10 @@ FK_EXPORT int fk_finish(fk_ctx *c) {
         const int rc = finish_exchange(c);
         return rc ? comm_fail(c, rc) : rc;  // collective: a failed rank fails the group
     }
+    return note_held(c, finish_local(c));
+}
+
+static int finish_local(fk_ctx *c) {
     if (c->G != 1)
         return set_err(FK_E_STATE, "fk_finish over %u ranks needs a communicator (fk_comm_init); or use "
                                    "fk_map/fk_map_emit/fk_reduce", c->G);
@@ -2948,19 +2787,8 @@ FK_EXPORT int fk_bin_sizes(fk_ctx *c, uint64_t *out) {
 
 // A bucket-major result made dense (fk_write_bins): the buckets' outputs compacted in bin order.
 static int materialize_dense(fk_ctx *c) {
-    if (!(c->gapped || c->ht_regions) || c->dense_ready) return FK_OK;
+    if (!c->gapped || c->dense_ready) return FK_OK;
     hipStream_t s = c->stream;
-    if (c->ht_regions) {  // the hash count's bin regions packed in bin order
-        FK_TRY(ensure(c->dense_keys, c->distinct * 8 * c->KW + 64));
-        FK_TRY(ensure(c->dense_counts, c->distinct * 4 + 64));
-        const uint64_t *d_km_base = c->lh_meta.as<uint64_t>() + (c->nlb + 1);
-        HIP_TRY(launch_ht_gather(c->KW, d_km_base, c->bin_off.as<uint64_t>(), c->nlb, c->lh_okeys.as<uint64_t>(),
-                                 c->lh_ocnt.as<uint32_t>(), c->dense_keys.as<uint64_t>(),
-                                 c->dense_counts.as<uint32_t>(), s));
-        HIP_TRY(hipStreamSynchronize(s));
-        c->dense_ready = true;
-        return FK_OK;
-    }
     FK_TRY(ensure(c->dense_keys, c->distinct * 8 * c->KW));
     FK_TRY(ensure(c->dense_counts, c->distinct * 4));
     HIP_TRY(launch_bucket_compact(c->KW, c->res_keys, c->out_counts.as<uint32_t>(), c->buckets.as<Bucket>(),
@@ -3001,13 +2829,6 @@ FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *count
     *n = (size_t)cnt;
     if (cnt == 0) return FK_OK;
     if (cap < cnt) return set_err(FK_E_RANGE, "bin %d has %llu k-mers, buffer holds %zu", bin, (unsigned long long)cnt, cap);
-    if (c->ht_regions && !c->dense_ready) {  // the bin's region of the hash count's output
-        const uint64_t r0 = c->h_ht_kbase[lb];
-        if (keys)
-            HIP_TRY(hipMemcpy(keys, c->lh_okeys.as<uint64_t>() + r0 * c->KW, cnt * 8 * c->KW, hipMemcpyDeviceToHost));
-        if (counts) HIP_TRY(hipMemcpy(counts, c->lh_ocnt.as<uint32_t>() + r0, cnt * 4, hipMemcpyDeviceToHost));
-        return FK_OK;
-    }
     if (c->gapped && !c->dense_ready) {
         FK_TRY(ensure(c->gather_keys, cnt * 8 * c->KW));
         FK_TRY(ensure(c->gather_counts, cnt * 4));

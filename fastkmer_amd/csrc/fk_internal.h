@@ -225,7 +225,7 @@ hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *bucket
 struct SubBucket {
     uint64_t src;   // first key in the split copy (skeys)
     uint64_t out;   // first output slot (the parent bucket's region of out_keys / out_counts)
-    uint64_t lo;    // every key lies in [lo, lo + 2^span)
+    uint64_t lo;    // every key lies in [lo, lo + 2^span) (the rank's group cut)
     uint32_t n, span;
 };
 struct SplitParent {
@@ -239,7 +239,7 @@ hipError_t launch_listed_sizes(const Bucket *buckets, const uint32_t *list0, uin
 hipError_t launch_bucket_split64(const BucketSrc &src, const Bucket *buckets, const uint32_t *list0, uint32_t n0,
                                  const uint32_t *list1, uint32_t n1, const uint64_t *sbase, uint64_t *skeys,
                                  SubBucket *subs, SplitParent *parents, unsigned int *counts, uint32_t *fb0,
-                                 uint32_t *fb1, uint32_t block_cap, hipStream_t s);
+                                 uint32_t *fb1, uint32_t block_cap, int k, int F, hipStream_t s);
 hipError_t launch_sub_count64_wave(const SubBucket *subs, uint64_t nsubs, const uint64_t *skeys, uint64_t *out_keys,
                                    uint32_t *out_counts, uint64_t *sub_unique, hipStream_t s, bool ordered = true);
 hipError_t launch_bucket_join(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
@@ -267,79 +267,6 @@ hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_
                                  uint64_t *dense_keys, uint32_t *dense_counts, hipStream_t s);
 hipError_t launch_bin_offsets(const uint64_t *flag_scan, const uint64_t *dense_off, uint32_t nlbins, int F,
                               uint64_t nbuckets, uint64_t *bin_off, hipStream_t s);
-
-// ---- hash count (extractKXmersHT)
-hipError_t launch_ht_insert(int W, int KW, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks, int k,
-                            const uint64_t *table_off, uint64_t *tkeys, uint32_t *tstate, uint32_t *tcounts,
-                            unsigned long long *fail, hipStream_t s);
-hipError_t launch_ht_flags(const uint32_t *tcounts, uint64_t nslots, uint32_t *flags, hipStream_t s);
-hipError_t launch_ht_compact(int KW, const uint64_t *tkeys, const uint32_t *tcounts, uint64_t nslots,
-                             const uint64_t *slot_scan, uint64_t *dense_keys, uint32_t *dense_counts,
-                             hipStream_t s);
-hipError_t launch_ht_bin_offsets(const uint64_t *slot_scan, const uint64_t *table_off, uint32_t nlbins,
-                                 uint64_t total, uint64_t *bin_off, hipStream_t s);
-
-// ---- hash count in LDS tables (fk_count_lds.inc), k <= 63 (64-bit keys up to k = 32, 128-bit above)
-struct LhGroup {          // one (local bin, fine value) group of records
-    uint64_t rec_begin;   // first record in the fine-partitioned array
-    uint64_t km_begin;    // first k-mer slot (prefix of the groups' k-mers): round-1 spill range
-    uint32_t rec_count, km_count;
-    uint32_t lbin, pad;
-};
-constexpr int LH_MAX_FLOG = 6;  // fine-hash bits in a record header
-hipError_t launch_fine_partition(int W, const uint64_t *rec, const Chunk *chunks, uint32_t nchunks,
-                                 const uint32_t *bcb, uint32_t nlb, const uint8_t *flog, const uint64_t *rec_base,
-                                 const uint64_t *km_base, const uint32_t *gbase, uint32_t *Hr, uint32_t *Hk,
-                                 uint64_t *off, LhGroup *groups, uint64_t *out, hipStream_t s);
-struct LhItem {            // one work item of a spill round: the keys of a parent range (the spill of a
-    uint64_t in_base;     // group, or of a parent of the previous round) whose salted key hash selects `sub`
-    uint64_t out_base;    // the parent's spill range (in_cnt slots, shared by its 2^slog sub-items)
-    uint32_t in_cnt, lbin, sub, slog;
-    uint32_t parent;      // spill cursor of the parent (sp_cnt[parent])
-    uint32_t pad;         // sub_off index of the parent's partitioned sub-ranges (k_ht_subpart), or
-                          // LH_NOPART: the item reads the whole parent range and filters by hash
-};
-constexpr uint32_t LH_NOPART = ~0u;
-constexpr int LH_SUB_MAXLOG = 12;  // parents split into at most 2^12 sub-items are pre-partitioned
-// spill-round pre-partition: parents[0..np) with pad != LH_NOPART (pad = sub_off base) -> their keys
-// copied to dst at the same offsets, grouped by the round's salted key hash & (2^slog - 1);
-// sub_off[pad + s] = the first key of sub-range s relative to in_base (2^slog + 1 entries)
-// the groups of round 1 that spilled (sp_cnt[g] > 0) as parents of the next round, in any order:
-// out[i] = {km_begin, 0, sp_cnt[g], lbin, 0, 0, 0, 0}; *n_out += their number
-hipError_t launch_ht_spill_list(const LhGroup *groups, const uint32_t *sp_cnt, uint32_t ngroups, LhItem *out,
-                                unsigned long long *n_out, hipStream_t s);
-// spill-round plan over np parents (one thread each): parents[p].slog = sub-item bits (2^slog
-// sub-items of about per_group keys); cnt = in_cnt, nsub = 2^slog, npad = 2^slog + 1 for a parent
-// pre-partitioned by k_ht_subpart (subpart != 0, 1 <= slog <= LH_SUB_MAXLOG), else 0
-hipError_t launch_ht_plan(LhItem *parents, uint32_t np, double per_group, int subpart, uint64_t *cnt, uint64_t *nsub,
-                          uint64_t *npad, hipStream_t s);
-// the round's items from the scanned plan (region = spill range, item_off, pad_off = sub_off base);
-// parents[p].pad = pad_off[p] or LH_NOPART
-hipError_t launch_ht_items(LhItem *parents, uint32_t np, const uint64_t *region, const uint64_t *item_off,
-                           const uint64_t *pad_off, const uint64_t *npad, LhItem *items, hipStream_t s);
-// the parents that spilled again (sp_cnt[p] > 0) as the next round's: {region[p], 0, sp_cnt[p], lbin}
-hipError_t launch_ht_next_parents(const LhItem *parents, uint32_t np, const uint64_t *region, const uint32_t *sp_cnt,
-                                  LhItem *out, unsigned long long *n_out, hipStream_t s);
-hipError_t launch_ht_subpart(int KW, const uint64_t *src, const LhItem *parents, uint32_t np, uint32_t salt,
-                             uint64_t *dst, uint32_t *sub_off, hipStream_t s);
-// items == null: round 1 over groups[0..n), sp_cnt[g] = keys group g spilled; else a spill round
-// over items[0..n), sp_cnt[parent] = the spill cursor of each parent (zeroed by the caller)
-hipError_t launch_ht_combine(int W, const uint64_t *src, const LhGroup *groups, const LhItem *items, uint32_t n,
-                             int k, uint32_t salt, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
-                             const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys, uint32_t *ocnt,
-                             hipStream_t s, int probe = 0, const uint64_t *psrc = nullptr,
-                             const uint32_t *sub_off = nullptr, uint32_t big_thr = 0);
-// 128-bit keys: round 1 of the groups of thr < k-mers <= hi (hi = 0: no bound; k_ht_big_list) in
-// 6144-slot tables
-hipError_t launch_ht_big_list(const LhGroup *groups, uint32_t ngroups, uint32_t thr, uint32_t hi, uint32_t *glist,
-                              unsigned long long *n_out, hipStream_t s);
-hipError_t launch_ht_combine128_big(const uint64_t *src, const LhGroup *groups, const uint32_t *glist, uint32_t n,
-                                    int k, uint64_t *spill, uint32_t *sp_cnt, unsigned long long *sp_total,
-                                    const uint64_t *bin_kbase, unsigned long long *bin_cnt, uint64_t *okeys,
-                                    uint32_t *ocnt, hipStream_t s);
-hipError_t launch_ht_gather(int KW, const uint64_t *bin_kbase, const uint64_t *bin_off, uint32_t nlb,
-                            const uint64_t *okeys, const uint32_t *ocnt, uint64_t *dkeys, uint32_t *dcnt,
-                            hipStream_t s);
 
 // ---- synthetic input
 hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);

@@ -339,8 +339,6 @@ hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWo
 #include "fk_expand2.inc"
 #include "fk_sort_radix.inc"
 #include "fk_compact.inc"
-#include "fk_count_hash.inc"
-#include "fk_count_lds.inc"
 #include "fk_synth.inc"
 #include "fk_format.inc"
 #include "fk_bin_signatures.inc"

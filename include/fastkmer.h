@@ -74,8 +74,8 @@ typedef struct fk_stats {
     double ms_h2d;             /* last fk_ingest: host-to-device copy, first segment issued to last landed */
     uint64_t fused_fallback;   /* why the fused kernel handed the input back: 1 long line, 2 text before the
                                   first header, 4 halo too short, 8 too many records in a tile (0: none) */
-    uint64_t ht_spilled;       /* useHT LDS tables: keys spilled over all rounds (each counted by a later round) */
-    uint64_t ht_rounds;        /* useHT LDS tables: rounds until every key was counted */
+    uint64_t ht_spilled;       /* unused (0): the useHT group tables are gone (useHT counts buckets) */
+    uint64_t ht_rounds;        /* unused (0) */
     /* multi-rank exchange inside the context (fk_comm_init*), last fk_finish */
     uint64_t xch_steps;        /* exchange steps (pieces sent during fk_ingest, the last piece, closing steps) */
     uint64_t xch_bytes_sent;   /* record bytes sent to other ranks */
@@ -85,10 +85,10 @@ typedef struct fk_stats {
     /* pieces counted while later ones were still being copied in / received (sorted count) */
     uint64_t pieces_counted;   /* staged pieces of the last fk_finish (0: one count of the whole input) */
     double ms_merge;           /* unused (0): staged pieces are counted once, never merged */
-    uint64_t precounted;       /* unused (0) */
+    uint64_t heavy_keys;       /* sorted count: k-mers in the buckets above the wave tier (split or block / big) */
     uint64_t block_buckets;    /* buckets above the wave tier of at most 2048 keys (mid wave tier, block kernel) */
     uint64_t big_buckets;      /* buckets above 2048 keys (the big-table kernel, then the large path) */
-    uint64_t ht_big_groups;    /* useHT, k > 32: groups counted in the 6144-slot tables */
+    uint64_t ht_big_groups;    /* unused (0) */
     uint64_t split_buckets;    /* k <= 32: buckets above the wave tier split into wave-sized sub-buckets */
     uint64_t sub_buckets;      /* ... into this many sub-buckets (the wave tier counted them) */
 } fk_stats;

@@ -101,7 +101,7 @@ def test_piece_counts_fallback_counts_whole_input(small_pieces):
 @pytest.mark.parametrize("k,m,read_len", [(28, 10, 100), (55, 12, 150)])
 def test_piece_counts_hash_mode_staged(small_pieces, k, m, read_len):
     # useHT=1 stages its pieces like the sorted count; the wave tiers emit table order
-    fasta = fk.synth_fasta(20_000, read_len, 400_000, seed=0xA5 + k)
+    fasta = fk.synth_fasta(30_000 if read_len == 100 else 20_000, read_len, 400_000, seed=0xA5 + k)
     kc = count_pinned(fasta, k, m, use_ht=True)
     assert kc.stats()["pieces_counted"] == 4
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, k, m, 2048), ordered=False)
