@@ -369,6 +369,11 @@ struct fk_ctx {
 
     fk::Comm *comm = nullptr;
     hipStream_t comm_stream = nullptr;
+    // staging of received segments on its own stream (each waits for its step's transfer, so the map
+    // stream never does) with its own scan workspace; the count waits for it
+    hipStream_t xstage = nullptr;
+    hipEvent_t xstage_ev = nullptr;
+    ScanWorkspace ws_x;
     hipEvent_t emit_ev = nullptr;                // map stream: a piece's send records are written
     std::vector<hipEvent_t> xev;                 // comm stream: begin / end of every piece's transfer
     uint64_t piece_bytes = 512ull << 20;         // FASTKMER_PIECE_BYTES: FASTA bytes per piece (1 GB with a
@@ -624,6 +629,9 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
         if (e) (void)hipEventDestroy(e);
     if (c->emit_ev) (void)hipEventDestroy(c->emit_ev);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->xstage) (void)hipStreamSynchronize(c->xstage), (void)hipStreamDestroy(c->xstage);
+    if (c->xstage_ev) (void)hipEventDestroy(c->xstage_ev);
+    if (c->ws_x.ptr) (void)hipFree(c->ws_x.ptr);
     c->dest.release_all();
     c->part.release_all();
     c->binhist.release_all();
@@ -771,6 +779,7 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         if (c->comm) {
             if (c->xch.open) return set_err(FK_E_STATE, "fk_ingest: the previous job's exchange is unfinished (fk_finish)");
             HIP_TRY(hipStreamSynchronize(c->comm_stream));
+            HIP_TRY(hipStreamSynchronize(c->xstage));
             xch_reset(c);
         }
         HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
@@ -1619,7 +1628,10 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         c->stats.big_buckets = ntier[1];
         hipStream_t ts = s;
         uint64_t nlarge = 0;
-        if (c->KW == 1 && (ntier[0] || ntier[1])) {
+#ifndef FK_SPLIT_HEAVY
+#define FK_SPLIT_HEAVY 1  // A/B builds (build_variant "nosplit", -DFK_SPLIT_HEAVY=0): no heavy-bucket split
+#endif
+        if (FK_SPLIT_HEAVY && c->KW == 1 && (ntier[0] || ntier[1])) {
             // 64-bit keys: the buckets above the wave tier split into wave-sized sub-buckets by the key
             // bits below their common prefix, counted by the wave tier and joined back; the buckets
             // with a sub-bucket too large for a wave keep the block / big-table kernels
@@ -1669,6 +1681,11 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     hb[cl] += 1, hk[cl] += n;
                     if (isfb[j]) hf[cl] += 1, hfk[cl] += n;
                 }
+                unsigned long long rk[4];
+                HIP_TRY(hipDeviceSynchronize());
+                HIP_TRY(rank_probe_read(rk, true));
+                fprintf(stderr, "probe_rank (wave tier, before the split): iterations %llu keys %llu buckets %llu "
+                        "wall (small groups) %llu\n", rk[0], rk[1], rk[2], rk[3]);
                 fprintf(stderr, "probe_split: listed %u keys %llu subs %u fallbacks %u + %u\n", nl,
                         (unsigned long long)base[nl], nsub, nfb0, nfb1);
                 for (int cl = 0; cl < 40; ++cl)
@@ -2342,6 +2359,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
             want = std::max<uint64_t>(want, (uint64_t)((double)want * (double)c->xch.expect_bytes / covered * 1.1));
         }
         HIP_TRY(hipStreamSynchronize(cs));
+        HIP_TRY(hipStreamSynchronize(c->xstage));  // staged expansions may still read the old buffer
         FK_TRY(grow_keep(c->xrecv, want * rb, c->xch.recv_used * rb, s));
     }
     const size_t step = (size_t)c->xch.pieces;
@@ -2410,11 +2428,26 @@ static int segment_ranges(fk_ctx *c, size_t s0, size_t s1, std::vector<std::vect
 // With a communicator and staged pieces: expands the received segments [segs_counted, s1) as one
 // staged piece (they arrive grouped by local bin: no partition), once the comm stream has
 // delivered them.  `frac` = their estimated fraction of what this rank receives in the job.
+// The context's stream and scan workspace swapped for the staging stream's while a staging step is
+// queued (the expansion code queues on c->stream).
+struct StageStream {
+    fk_ctx *c;
+    explicit StageStream(fk_ctx *c_) : c(c_) {
+        std::swap(c->stream, c->xstage);
+        std::swap(c->ws, c->ws_x);
+    }
+    ~StageStream() {
+        std::swap(c->stream, c->xstage);
+        std::swap(c->ws, c->ws_x);
+    }
+};
+
 static int xch_stage_segments(fk_ctx *c, size_t s1, double frac) {
     if (s1 <= c->segs_counted) return FK_OK;
     const uint32_t p = c->st_np;
     if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
-    hipStream_t s = c->stream;
+    StageStream ss_(c);
+    hipStream_t s = c->stream;  // the staging stream
     // the chunk table goes up through the pinned staging buffer: the last upload from it is done
     HIP_TRY(hipStreamSynchronize(s));
     const uint64_t step = c->xch.segs[s1 - 1].step;
@@ -2479,11 +2512,11 @@ static int xch_maybe_piece(fk_ctx *c) {
     const uint64_t t0 = c->xch.tiles_sent, nt = c->pm_tiles - t0;
     const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
     c->xch.tiles_sent = c->pm_tiles;
-    const size_t before = c->xch.segs.size();
     const int rc = xch_step(c, &src, 0);
     if (rc) return comm_fail(c, rc);
-    // the records of the earlier steps are counted (staged: expanded) while this step's are on the wire
-    if (staged_ok(c) && !c->pieces_void && before > c->segs_counted) FK_TRY(xch_maybe_stage(c, before));
+    // the received segments are expanded (staged) on the staging stream as soon as their transfer
+    // ends, this step's included, while the map stream goes on
+    if (staged_ok(c) && !c->pieces_void) FK_TRY(xch_maybe_stage(c, c->xch.segs.size()));
     return FK_OK;
 }
 
@@ -2511,6 +2544,8 @@ static int finish_exchange(fk_ctx *c) {
     if (rc) return comm_fail(c, rc);
     HIP_TRY(hipEventRecord(c->ev[4], cs));  // every rank's records have landed
     HIP_TRY(hipStreamWaitEvent(s, c->ev[4], 0));
+    HIP_TRY(hipEventRecord(c->xstage_ev, c->xstage));  // and the staged expansions queued so far are done
+    HIP_TRY(hipStreamWaitEvent(s, c->xstage_ev, 0));
     uint64_t nrecv = 0;
     for (const auto &g : c->xch.segs)
         for (uint64_t n : g.rec) nrecv += n;
@@ -2521,6 +2556,8 @@ static int finish_exchange(fk_ctx *c) {
             for (size_t i = c->segs_counted; i < c->xch.segs.size(); ++i)
                 for (uint64_t n : c->xch.segs[i].rec) recs += n;
             FK_TRY(xch_stage_segments(c, c->xch.segs.size(), nrecv ? (double)recs / (double)nrecv : 0.0));
+            HIP_TRY(hipEventRecord(c->xstage_ev, c->xstage));
+            HIP_TRY(hipStreamWaitEvent(s, c->xstage_ev, 0));
         }
         FK_TRY(staged_count(c));
     } else {
@@ -2580,6 +2617,8 @@ static int finish_local(fk_ctx *c) {
 static int attach_comm(fk_ctx *c, fk::Comm *comm) {
     DeviceGuard dg_(c->device);
     if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (!c->xstage) HIP_TRY(hipStreamCreateWithFlags(&c->xstage, hipStreamNonBlocking));
+    if (!c->xstage_ev) HIP_TRY(hipEventCreateWithFlags(&c->xstage_ev, hipEventDisableTiming));
     if (!c->emit_ev) HIP_TRY(hipEventCreateWithFlags(&c->emit_ev, hipEventDisableTiming));
     c->comm = comm;
     if (!c->piece_bytes_set) c->piece_bytes = 1ull << 30;

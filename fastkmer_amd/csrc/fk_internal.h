@@ -105,6 +105,8 @@ uint64_t fm_span_bytes(int nth);
 uint32_t map_fused_tcap();
 // measurement build (-DFK_PROBES): the fused map's per-phase wave cycles summed since the last reset
 hipError_t map_fused_cycles(unsigned long long *out16, bool reset);
+// measurement build: the sorted wave tiers' rank loop -- [0] iterations, [1] keys ranked, [2] buckets
+hipError_t rank_probe_read(unsigned long long *out4, bool reset);
 uint32_t map_fused_cslot();
 uint32_t map_fused_vslot();  // split map: valid-stream slot words per tile (vslots)
 hipError_t launch_map_fused(int nth, int k, int m, const uint8_t *fa, uint64_t n, int more, uint64_t tile_begin,

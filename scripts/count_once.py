@@ -4,7 +4,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa
 import fastkmer_amd as fk
 kc = fk.KmerCounter(28, 10, 3, int(os.environ.get('FK_B', '2048')), use_ht=os.environ.get('FK_HT', '0') == '1')
-kc.synth_device(1_000_000_000 // 114, 100, int(os.environ.get('FK_GENOME', '100000000')), seed=0x5EED)
+kc.synth_device(int(os.environ.get('FK_BYTES', '1000000000')) // 114, 100, int(os.environ.get('FK_GENOME', '100000000')), seed=0x5EED)
 for i in range(3):
     kc.finish()
 st = kc.stats()

@@ -1,13 +1,11 @@
 #!/bin/bash
-# Round 5 third GPU call: heavy buckets cut by sample splitters; useHT on the bucket path only (group
-# tables removed); the staged count's output over `mid` and trimmed allocation slack.  Tests, the
-# split's size classes at configs[2] (probe library), configs[2] sorted / useHT / nosplit A/B, the
-# one-rank exchange, the two-rank configs[2] rehearsal on one GPU (footprint), kernel stats.
+# Round 5 fourth GPU call: the heavy-split parity cases; configs[2] / [1] with and without the heavy
+# split (lib_nosplit = -DFK_SPLIT_HEAVY=0); useHT; the one-rank exchange with staging on its own
+# stream; the two-rank configs[2] rehearsal on one GPU (footprint); kernel stats; PMC of the tiers.
 set -o pipefail
-R="$GRAFT_REPO_ROOT"; O=$R/gpurun_out/r05c; mkdir -p $O
+R="$GRAFT_REPO_ROOT"; O=$R/gpurun_out/r05d; mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_gpu_wave.py tests/test_gpu_hash.py tests/test_gpu_pieces.py tests/test_gpu_write.py \
-  "tests/test_gpu_parity.py::test_heavy_bucket_split_vs_oracle" tests/test_gpu_comm.py \
+timeout -k 10 300 python -u -m pytest "tests/test_gpu_parity.py::test_heavy_bucket_split_vs_oracle" tests/test_gpu_comm.py \
   -m gpu -v --maxfail 4 --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; grep -E "FAILED|ERROR" $O/tests.log | head -20
 [[ $rc -gt 1 ]] && { echo "tests rc=$rc"; tail -30 $O/tests.log; exit 1; }
@@ -15,21 +13,18 @@ B="--steps 5 --warmup 2 --no-cpu-baseline --no-device-leg"
 run() {  # name, env..., -- bench args
   local name=$1; shift
   timeout -k 10 240 env "$@" > $O/$name.json 2> $O/$name.err || { echo "$name failed"; tail -20 $O/$name.err; return 1; }
-  python - "$O/$name.json" "$name" <<'EOF'
+  python - "$O/$name.json" "$name" <<'PYEOF'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[2], round(d["ms_per_step"], 2), {k: round(v, 2) for k, v in d["stages_ms"].items()}, d.get("buckets_rank0"))
-EOF
+PYEOF
 }
-AB="import sys, runpy; sys.path.insert(0, 'ab/nosplit'); import fastkmer_amd; sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('bench.py', run_name='__main__')"
-timeout -k 10 240 env FASTKMER_LIB=$R/fastkmer_amd/lib_probes/libfastkmer.so FASTKMER_HOST_TRACE=1 python -u bench.py \
-  --workload c3 --steps 1 --warmup 0 --no-cpu-baseline --no-device-leg > $O/probe_split.json 2> $O/probe_split.err \
-  || { echo "probe failed"; tail -20 $O/probe_split.err; exit 1; }
-grep probe_split $O/probe_split.err | tail -25
+NS=FASTKMER_LIB=$R/fastkmer_amd/lib_nosplit/libfastkmer.so
 run c3_sorted X=1 python -u bench.py --workload c3 $B || exit 1
-run c3_sorted_nosplit X=1 python -u -c "$AB" --workload c3 $B || exit 1
-run c3_ht X=1 python -u bench.py --workload c3 --use-ht $B || exit 1
+run c3_sorted_nosplit $NS python -u bench.py --workload c3 $B || exit 1
 run c2_sorted X=1 python -u bench.py $B || exit 1
+run c2_sorted_nosplit $NS python -u bench.py $B || exit 1
+run c3_ht X=1 python -u bench.py --workload c3 --use-ht $B || exit 1
 run c3_rehearse1 FASTKMER_BENCH_MEMINFO=1 python -u bench.py --rehearse-local 1 --workload c3 $B || exit 1
 grep meminfo $O/c3_rehearse1.err
 run c3_rehearse2 FASTKMER_BENCH_MEMINFO=1 python -u bench.py --rehearse-local 2 --workload c3 --bytes-per-gpu 6250000000 \
@@ -38,6 +33,7 @@ grep meminfo $O/c3_rehearse2.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 $R/bench.py --workload c3 \
   --steps 3 --warmup 1 --no-cpu-baseline --no-device-leg > $O/prof_c3.json 2> $O/prof_c3.err || { echo "prof failed"; tail -20 $O/prof_c3.err; exit 1; }
-find $O/prof_c3 -name "*kernel_stats.csv" | head -3
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_xch1 -o run -- python3 $R/bench.py --workload c3 \
   --rehearse-local 1 --steps 3 --warmup 1 --no-cpu-baseline --no-device-leg > $O/prof_xch1.json 2> $O/prof_xch1.err || { echo "prof xch failed"; tail -20 $O/prof_xch1.err; exit 1; }
+cd $R
+bash scripts/r05_pmc_wave.sh r05d || exit 1

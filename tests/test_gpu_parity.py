@@ -613,7 +613,7 @@ def test_grouped_emit_with_owners_set_after_map(k, m, B):
 @pytest.mark.parametrize("k,m,staged", [(28, 10, False), (32, 11, False), (21, 7, False), (28, 10, True)])
 def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged):
     # buckets above the wave tier (cells of a few thousand keys, FASTKMER_DEBUG_CELL_TARGET) split into
-    # wave-sized sub-buckets by the key bits below their common prefix, counted by the wave tier and
+    # wave-sized sub-buckets by sampled splitters (~256 keys each), counted by the wave tier and
     # joined back in place -- from one key array and from staged pieces (a pinned ingest in 512 KB
     # pieces); k = 32 keys use all 64 bits; repeated reads leave sub-buckets too large for a wave, which
     # keep the block / big-table path (pieces need the fused map: k=28 m=10 or k=55 m=12)
@@ -634,7 +634,7 @@ def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged):
     else:
         kc = run_counter(fasta, k, m, 3, 16)
     st = kc.stats()
-    assert st["split_buckets"] > 100 and st["sub_buckets"] > 8 * st["split_buckets"], st
+    assert st["split_buckets"] > 100 and st["sub_buckets"] > 3 * st["split_buckets"], st
     assert st["split_buckets"] < st["block_buckets"] + st["big_buckets"], st  # the repeats fall back
     ref = oracle.OracleResult(fasta, k, m, 16, threads=4)
     assert st["kmers"] == ref.total_kmers
