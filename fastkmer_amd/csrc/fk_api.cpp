@@ -376,8 +376,8 @@ struct fk_ctx {
     ScanWorkspace ws_x;
     hipEvent_t emit_ev = nullptr;                // map stream: a piece's send records are written
     std::vector<hipEvent_t> xev;                 // comm stream: begin / end of every piece's transfer
-    uint64_t piece_bytes = 512ull << 20;         // FASTKMER_PIECE_BYTES: FASTA bytes per piece (1 GB with a
-                                                 // communicator)
+    uint64_t piece_bytes = 512ull << 20;         // FASTKMER_PIECE_BYTES: FASTA bytes per piece (with a
+                                                 // communicator: a fifth of a known job, 128 MB .. 1 GB)
     bool piece_bytes_set = false;
     uint64_t ingest_seg = 32ull << 20;           // FASTKMER_INGEST_SEG: H2D segment of a pinned source
     DevBuf xsend, xrecv;                         // send ring (pieces in flight), received records
@@ -826,7 +826,17 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     // with a communicator, every piece of mapped tiles is exchanged while later ones land
     const bool pieces = c->comm && c->pm_active;
     // the job's size: this call's when it holds the whole input, else what fk_ingest_reserve announced
-    if (pieces && fresh) c->xch.expect_bytes = last ? n : c->reserve_bytes;
+    if (pieces && fresh) {
+        c->xch.expect_bytes = last ? n : c->reserve_bytes;
+        // a job of known size goes out in about XCH_STEPS steps (at most 1 GB, at least 128 MB each):
+        // every step but the last moves while later bytes are copied in (one 1 GB step for a 1 GB job
+        // would leave the whole exchange after the last byte)
+        constexpr uint64_t XCH_STEPS = 5;
+        if (!c->piece_bytes_set)
+            c->piece_bytes = c->xch.expect_bytes
+                                 ? std::min<uint64_t>(1ull << 30, std::max<uint64_t>(128ull << 20, c->xch.expect_bytes / XCH_STEPS))
+                                 : 1ull << 30;
+    }
     if (fresh) {
         c->job_bytes = last ? n : c->reserve_bytes;
         c->reserve_bytes = 0;
@@ -1631,99 +1641,105 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
 #ifndef FK_SPLIT_HEAVY
 #define FK_SPLIT_HEAVY 1  // A/B builds (build_variant "nosplit", -DFK_SPLIT_HEAVY=0): no heavy-bucket split
 #endif
-        if (FK_SPLIT_HEAVY && c->KW == 1 && (ntier[0] || ntier[1])) {
-            // 64-bit keys: the buckets above the wave tier split into wave-sized sub-buckets by the key
-            // bits below their common prefix, counted by the wave tier and joined back; the buckets
-            // with a sub-bucket too large for a wave keep the block / big-table kernels
+        if (c->KW == 1 && (ntier[0] || ntier[1])) {
+            // 64-bit keys: the buckets above the wave tier split into wave-sized sub-buckets by sampled
+            // splitters, counted by the wave tier and joined back; the buckets with a sub-bucket too
+            // large for a wave keep the block / big-table kernels
             const uint32_t nl = ntier[0] + ntier[1];
-            const uint64_t maxsub = listed_keys / 64 + nl + 64;  // 2^b < 2 n / SPL_KEYS sub-buckets per bucket
-            FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
-            FK_TRY(ensure(c->sp_keys, listed_keys * 8));
-            FK_TRY(ensure(c->sp_subs, maxsub * sizeof(SubBucket)));
-            FK_TRY(ensure(c->sp_par, (uint64_t)nl * sizeof(SplitParent)));
-            FK_TRY(ensure(c->sp_uniq, maxsub * 8));
-            FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
             const uint32_t *l1 = lists + nbuckets;
-            uint32_t *fb = c->sp_fb.as<uint32_t>();
-            unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
-            HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
-                                        c->sp_base.as<uint64_t>(), s));
-            HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
-                                      c->sp_base.as<uint64_t>() + nl, c->ws, s));
-            HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
-                                          c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
-                                          c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb, fb + nl,
-                                          cap, k, F, s));
-            HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipEventRecord(c->tier_ev, s));
-            HIP_TRY(hipEventSynchronize(c->tier_ev));
-            const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
-            const uint32_t nsub = sc[0], nfb0 = sc[1], nfb1 = sc[2];
-            htrace("sorted: split counts read");
+            uint32_t *fb0 = lists, *fb1 = lists + nbuckets;  // the fallbacks (no split: every listed bucket)
+            uint32_t nfb0 = ntier[0], nfb1 = ntier[1];
+            if (FK_SPLIT_HEAVY) {
+                const uint64_t maxsub = listed_keys / 64 + nl + 64;  // >= ceil(n / SPL_TGT) sub-buckets per bucket
+                FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
+                FK_TRY(ensure(c->sp_keys, listed_keys * 8));
+                FK_TRY(ensure(c->sp_subs, maxsub * sizeof(SubBucket)));
+                FK_TRY(ensure(c->sp_par, (uint64_t)nl * sizeof(SplitParent)));
+                FK_TRY(ensure(c->sp_uniq, maxsub * 8));
+                FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
+                uint32_t *fb = c->sp_fb.as<uint32_t>();
+                unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
+                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                                            c->sp_base.as<uint64_t>(), s));
+                HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
+                                          c->sp_base.as<uint64_t>() + nl, c->ws, s));
+                HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                                              c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
+                                              c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb, fb + nl,
+                                              cap, k, F, s));
+                HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipEventRecord(c->tier_ev, s));
+                HIP_TRY(hipEventSynchronize(c->tier_ev));
+                const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
+                const uint32_t nsub = sc[0];
+                nfb0 = sc[1], nfb1 = sc[2], fb0 = fb, fb1 = fb + nl;
+                htrace("sorted: split counts read");
 #ifdef FK_PROBES
-            if (getenv("FASTKMER_HOST_TRACE")) {  // the listed buckets by size class: buckets, keys, fallbacks
-                std::vector<uint64_t> base((size_t)nl + 1);
-                std::vector<uint32_t> f(2 * (size_t)nl);
-                HIP_TRY(hipMemcpy(base.data(), c->sp_base.p, base.size() * 8, hipMemcpyDeviceToHost));
-                HIP_TRY(hipMemcpy(f.data(), fb, f.size() * 4, hipMemcpyDeviceToHost));
-                std::vector<uint32_t> h_l((size_t)nl);
-                HIP_TRY(hipMemcpy(h_l.data(), lists, (size_t)ntier[0] * 4, hipMemcpyDeviceToHost));
-                HIP_TRY(hipMemcpy(h_l.data() + ntier[0], l1, (size_t)ntier[1] * 4, hipMemcpyDeviceToHost));
-                std::unordered_map<uint32_t, uint32_t> pos;
-                for (uint32_t j = 0; j < nl; ++j) pos[h_l[j]] = j;
-                uint64_t hb[40] = {}, hk[40] = {}, hf[40] = {}, hfk[40] = {};
-                std::vector<char> isfb(nl, 0);
-                for (uint32_t j = 0; j < nfb0; ++j) isfb[pos[f[j]]] = 1;
-                for (uint32_t j = 0; j < nfb1; ++j) isfb[pos[f[nl + j]]] = 1;
-                for (uint32_t j = 0; j < nl; ++j) {
-                    const uint64_t n = base[j + 1] - base[j];
-                    const int cl = 63 - __builtin_clzll(n | 1);
-                    hb[cl] += 1, hk[cl] += n;
-                    if (isfb[j]) hf[cl] += 1, hfk[cl] += n;
+                if (getenv("FASTKMER_HOST_TRACE")) {  // the listed buckets by size class: buckets, keys, fallbacks
+                    std::vector<uint64_t> base((size_t)nl + 1);
+                    std::vector<uint32_t> f(2 * (size_t)nl);
+                    HIP_TRY(hipMemcpy(base.data(), c->sp_base.p, base.size() * 8, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipMemcpy(f.data(), fb, f.size() * 4, hipMemcpyDeviceToHost));
+                    std::vector<uint32_t> h_l((size_t)nl);
+                    HIP_TRY(hipMemcpy(h_l.data(), lists, (size_t)ntier[0] * 4, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipMemcpy(h_l.data() + ntier[0], l1, (size_t)ntier[1] * 4, hipMemcpyDeviceToHost));
+                    std::unordered_map<uint32_t, uint32_t> pos;
+                    for (uint32_t j = 0; j < nl; ++j) pos[h_l[j]] = j;
+                    uint64_t hb[40] = {}, hk[40] = {}, hf[40] = {}, hfk[40] = {};
+                    std::vector<char> isfb(nl, 0);
+                    for (uint32_t j = 0; j < nfb0; ++j) isfb[pos[f[j]]] = 1;
+                    for (uint32_t j = 0; j < nfb1; ++j) isfb[pos[f[nl + j]]] = 1;
+                    for (uint32_t j = 0; j < nl; ++j) {
+                        const uint64_t n = base[j + 1] - base[j];
+                        const int cl = 63 - __builtin_clzll(n | 1);
+                        hb[cl] += 1, hk[cl] += n;
+                        if (isfb[j]) hf[cl] += 1, hfk[cl] += n;
+                    }
+                    unsigned long long rk[4];
+                    HIP_TRY(hipDeviceSynchronize());
+                    HIP_TRY(rank_probe_read(rk, true));
+                    fprintf(stderr, "probe_rank (wave tier, before the split): iterations %llu keys %llu buckets %llu "
+                            "wall (small groups) %llu\n", rk[0], rk[1], rk[2], rk[3]);
+                    fprintf(stderr, "probe_split: listed %u keys %llu subs %u fallbacks %u + %u\n", nl,
+                            (unsigned long long)base[nl], nsub, nfb0, nfb1);
+                    for (int cl = 0; cl < 40; ++cl)
+                        if (hb[cl])
+                            fprintf(stderr, "probe_split: n in [2^%d, 2^%d): buckets %llu keys %llu fallback buckets %llu keys %llu\n",
+                                    cl, cl + 1, (unsigned long long)hb[cl], (unsigned long long)hk[cl],
+                                    (unsigned long long)hf[cl], (unsigned long long)hfk[cl]);
                 }
-                unsigned long long rk[4];
-                HIP_TRY(hipDeviceSynchronize());
-                HIP_TRY(rank_probe_read(rk, true));
-                fprintf(stderr, "probe_rank (wave tier, before the split): iterations %llu keys %llu buckets %llu "
-                        "wall (small groups) %llu\n", rk[0], rk[1], rk[2], rk[3]);
-                fprintf(stderr, "probe_split: listed %u keys %llu subs %u fallbacks %u + %u\n", nl,
-                        (unsigned long long)base[nl], nsub, nfb0, nfb1);
-                for (int cl = 0; cl < 40; ++cl)
-                    if (hb[cl])
-                        fprintf(stderr, "probe_split: n in [2^%d, 2^%d): buckets %llu keys %llu fallback buckets %llu keys %llu\n",
-                                cl, cl + 1, (unsigned long long)hb[cl], (unsigned long long)hk[cl],
-                                (unsigned long long)hf[cl], (unsigned long long)hfk[cl]);
-            }
 #endif
-            if (nsub > maxsub) return set_err(FK_E_DEVICE, "bucket split: %u sub-buckets of at most %llu", nsub,
-                                              (unsigned long long)maxsub);
-            HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
-                                            okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                            c->sp_uniq.as<uint64_t>(), s, ordered));
-            HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
-                                       c->sp_par.as<SplitParent>(), c->sp_subs.as<SubBucket>(),
-                                       c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                       B.bucket_unique->as<uint64_t>(), s));
-            c->stats.split_buckets = nl - nfb0 - nfb1;
-            c->stats.sub_buckets = nsub;
+                if (nsub > maxsub) return set_err(FK_E_DEVICE, "bucket split: %u sub-buckets of at most %llu", nsub,
+                                                  (unsigned long long)maxsub);
+                HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
+                                                okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                c->sp_uniq.as<uint64_t>(), s, ordered));
+                HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                                           c->sp_par.as<SplitParent>(), c->sp_subs.as<SubBucket>(),
+                                           c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                           B.bucket_unique->as<uint64_t>(), s));
+                c->stats.split_buckets = nl - nfb0 - nfb1;
+                c->stats.sub_buckets = nsub;
+            }
             if (nfb0)
                 HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nfb0, k, okb.as<uint64_t>(),
                                               B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                              c->misc.as<unsigned long long>() + 1, cap, 99, fb, s));
+                                              c->misc.as<unsigned long long>() + 1, cap, 99, fb0, s));
             if (nfb1) {
                 // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
                 HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfb1, k, okb.as<uint64_t>(),
                                                   B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                  c->misc.as<unsigned long long>() + 2, fb + nl, s));
+                                                  c->misc.as<unsigned long long>() + 2, fb1, s));
                 HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
             }
-            if (nlarge) {
-                FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+            if (nlarge) {  // scratch for the listed buckets' keys only, taken by a cursor
+                FK_TRY(ensure(c->scratch, listed_keys * 8 * c->KW));
+                HIP_TRY(hipMemsetAsync(c->misc.as<unsigned long long>() + 6, 0, 8, s));
                 HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), nfb1, k,
                                                  c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                 fb + nl, s));
+                                                 fb1, s, c->misc.as<unsigned long long>() + 6));
             }
         } else if (ntier[0] || ntier[1]) {
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
@@ -1737,12 +1753,13 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                        B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
                                        lists, ts, WAVE128_MID_CAP));
             nlarge = ntier[1];
-            if (nlarge) {
-                FK_TRY(ensure(c->scratch, total_kmers * 8 * c->KW));
+            if (nlarge) {  // scratch for the listed buckets' keys only, taken by a cursor
+                FK_TRY(ensure(c->scratch, listed_keys * 8 * c->KW));
+                HIP_TRY(hipMemsetAsync(c->misc.as<unsigned long long>() + 6, 0, 8, ts));
                 HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), ntier[1], k,
                                                  c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                 lists + nbuckets, ts));
+                                                 lists + nbuckets, ts, c->misc.as<unsigned long long>() + 6));
             }
         }
         c->stats.oversize_buckets = nlarge;

@@ -263,7 +263,8 @@ hipError_t launch_bucket_count128_wave_mid(const BucketSrc &src, const Bucket *b
                                            uint64_t *bucket_unique, hipStream_t s, bool ordered = true);
 hipError_t launch_bucket_sort_large(int KW, const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                     uint64_t *scratch, uint64_t *out_keys, uint32_t *out_counts,
-                                    uint64_t *bucket_unique, const uint32_t *list, hipStream_t s);
+                                    uint64_t *bucket_unique, const uint32_t *list, hipStream_t s,
+                                    unsigned long long *scratch_cursor = nullptr);
 hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_t *out_counts,
                                  const Bucket *buckets, uint64_t nbuckets, const uint64_t *dense_off,
                                  uint64_t *dense_keys, uint32_t *dense_counts, hipStream_t s);
