@@ -377,7 +377,7 @@ struct fk_ctx {
     hipEvent_t emit_ev = nullptr;                // map stream: a piece's send records are written
     std::vector<hipEvent_t> xev;                 // comm stream: begin / end of every piece's transfer
     uint64_t piece_bytes = 512ull << 20;         // FASTKMER_PIECE_BYTES: FASTA bytes per piece (with a
-                                                 // communicator: a fifth of a known job, 128 MB .. 1 GB)
+                                                 // communicator: a tenth of a known job, 128 MB .. 1 GB)
     bool piece_bytes_set = false;
     uint64_t ingest_seg = 32ull << 20;           // FASTKMER_INGEST_SEG: H2D segment of a pinned source
     DevBuf xsend, xrecv;                         // send ring (pieces in flight), received records
@@ -830,8 +830,10 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         c->xch.expect_bytes = last ? n : c->reserve_bytes;
         // a job of known size goes out in about XCH_STEPS steps (at most 1 GB, at least 128 MB each):
         // every step but the last moves while later bytes are copied in (one 1 GB step for a 1 GB job
-        // would leave the whole exchange after the last byte)
-        constexpr uint64_t XCH_STEPS = 5;
+        // would leave the whole exchange after the last byte), and the staging cuts (st_cuts) fall on
+        // step ends (1 GB steps of a 6.25 GB job staged 5-6 GB after the last byte: 11 ms of expansion
+        // in the tail, profiles/r05d_xch1_c3_tail.txt)
+        constexpr uint64_t XCH_STEPS = 10;
         if (!c->piece_bytes_set)
             c->piece_bytes = c->xch.expect_bytes
                                  ? std::min<uint64_t>(1ull << 30, std::max<uint64_t>(128ull << 20, c->xch.expect_bytes / XCH_STEPS))
@@ -1642,10 +1644,16 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
 #define FK_SPLIT_HEAVY 1  // A/B builds (build_variant "nosplit", -DFK_SPLIT_HEAVY=0): no heavy-bucket split
 #endif
         if (c->KW == 1 && (ntier[0] || ntier[1])) {
-            // 64-bit keys: the buckets above the wave tier split into wave-sized sub-buckets by sampled
+            // 64-bit keys: the buckets above the block tier split into wave-sized sub-buckets by sampled
             // splitters, counted by the wave tier and joined back; the buckets with a sub-bucket too
-            // large for a wave keep the block / big-table kernels
-            const uint32_t nl = ntier[0] + ntier[1];
+            // large for a wave keep the big-table kernel.  The block tier (513..2048 keys) keeps its
+            // kernel: splitting it too measured the same at the configs[2] load and 0.35 ms slower at
+            // configs[1] (FK_SPLIT_BLOCK=1 builds it for A/B)
+#ifndef FK_SPLIT_BLOCK
+#define FK_SPLIT_BLOCK 0
+#endif
+            const uint32_t n0s = FK_SPLIT_BLOCK ? ntier[0] : 0u;
+            const uint32_t nl = n0s + ntier[1];
             const uint32_t *l1 = lists + nbuckets;
             uint32_t *fb0 = lists, *fb1 = lists + nbuckets;  // the fallbacks (no split: every listed bucket)
             uint32_t nfb0 = ntier[0], nfb1 = ntier[1];
@@ -1659,11 +1667,11 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
                 uint32_t *fb = c->sp_fb.as<uint32_t>();
                 unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
-                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, n0s, l1, ntier[1],
                                             c->sp_base.as<uint64_t>(), s));
                 HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
                                           c->sp_base.as<uint64_t>() + nl, c->ws, s));
-                HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, n0s, l1, ntier[1],
                                               c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
                                               c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb, fb + nl,
                                               cap, k, F, s));
@@ -1672,7 +1680,8 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 HIP_TRY(hipEventSynchronize(c->tier_ev));
                 const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
                 const uint32_t nsub = sc[0];
-                nfb0 = sc[1], nfb1 = sc[2], fb0 = fb, fb1 = fb + nl;
+                if (n0s) nfb0 = sc[1], fb0 = fb;
+                nfb1 = sc[2], fb1 = fb + nl;
                 htrace("sorted: split counts read");
 #ifdef FK_PROBES
                 if (getenv("FASTKMER_HOST_TRACE")) {  // the listed buckets by size class: buckets, keys, fallbacks
@@ -1681,13 +1690,13 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     HIP_TRY(hipMemcpy(base.data(), c->sp_base.p, base.size() * 8, hipMemcpyDeviceToHost));
                     HIP_TRY(hipMemcpy(f.data(), fb, f.size() * 4, hipMemcpyDeviceToHost));
                     std::vector<uint32_t> h_l((size_t)nl);
-                    HIP_TRY(hipMemcpy(h_l.data(), lists, (size_t)ntier[0] * 4, hipMemcpyDeviceToHost));
-                    HIP_TRY(hipMemcpy(h_l.data() + ntier[0], l1, (size_t)ntier[1] * 4, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipMemcpy(h_l.data(), lists, (size_t)n0s * 4, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipMemcpy(h_l.data() + n0s, l1, (size_t)ntier[1] * 4, hipMemcpyDeviceToHost));
                     std::unordered_map<uint32_t, uint32_t> pos;
                     for (uint32_t j = 0; j < nl; ++j) pos[h_l[j]] = j;
                     uint64_t hb[40] = {}, hk[40] = {}, hf[40] = {}, hfk[40] = {};
                     std::vector<char> isfb(nl, 0);
-                    for (uint32_t j = 0; j < nfb0; ++j) isfb[pos[f[j]]] = 1;
+                    for (uint32_t j = 0; j < sc[1]; ++j) isfb[pos[f[j]]] = 1;
                     for (uint32_t j = 0; j < nfb1; ++j) isfb[pos[f[nl + j]]] = 1;
                     for (uint32_t j = 0; j < nl; ++j) {
                         const uint64_t n = base[j + 1] - base[j];
@@ -1701,7 +1710,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     fprintf(stderr, "probe_rank (wave tier, before the split): iterations %llu keys %llu buckets %llu "
                             "wall (small groups) %llu\n", rk[0], rk[1], rk[2], rk[3]);
                     fprintf(stderr, "probe_split: listed %u keys %llu subs %u fallbacks %u + %u\n", nl,
-                            (unsigned long long)base[nl], nsub, nfb0, nfb1);
+                            (unsigned long long)base[nl], nsub, sc[1], nfb1);
                     for (int cl = 0; cl < 40; ++cl)
                         if (hb[cl])
                             fprintf(stderr, "probe_split: n in [2^%d, 2^%d): buckets %llu keys %llu fallback buckets %llu keys %llu\n",
@@ -1714,11 +1723,11 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
                                                 okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                                 c->sp_uniq.as<uint64_t>(), s, ordered));
-                HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, ntier[0], l1, ntier[1],
+                HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, n0s, l1, ntier[1],
                                            c->sp_par.as<SplitParent>(), c->sp_subs.as<SubBucket>(),
                                            c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                            B.bucket_unique->as<uint64_t>(), s));
-                c->stats.split_buckets = nl - nfb0 - nfb1;
+                c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
             if (nfb0)
