@@ -1464,7 +1464,7 @@ static SortedPlan sorted_plan(const fk_ctx *c, uint64_t max_bin_kmers) {
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     if (!two_level) F = std::min(F, MAX_FINE_BITS - 1);  // one-level scatter: 8 << F bytes of LDS <= 128 KB
     F = std::min(F, 2 * k);
-    // FASTKMER_EXPAND_LEVELS (k <= 32): 1 one-level scatter, 2 (default) super-cells then cells
+    // k <= 63: two levels (super-cells, then cells; one level measured slower, DESIGN.md §4 "Count" 7);
     // cells per super-cell: 2^5 up to F = 13, 2^6 above (measured at configs[1] and at 8x larger bins)
     const uint32_t wave_cap = c->KW == 1 ? WAVE_BUCKET_CAP : WAVE128_BUCKET_CAP;
     const int F2 = std::min(F, std::max(5, std::min(6, F - 8))), F1 = F - F2;
@@ -2125,9 +2125,8 @@ static int staged_expand_chunks(fk_ctx *c, uint32_t nchunks, const std::vector<u
         if (!c->st_plan.tiered || !c->st_plan.two_level)
             return set_err(FK_E_STATE, "staged pieces need the tiered two-level count");
     }
-    // a small piece (FASTKMER_STAGED_ONE_LEVEL: below this fraction of the job; default none) is
-    // scattered to its cells in one pass.  Off since level 2 sizes its workgroups to the keys per
-    // super-cell (a 15 % piece: 1.14 ms one-pass against ~0.75 ms for both levels).
+    // every piece takes both levels (level 2 sizes its workgroups to the keys per super-cell: a 15 %
+    // piece 0.75 ms against 1.14 for a one-pass scatter)
     SortedPlan pl = c->st_plan;
     HIP_TRY(hipEventRecord(c->st_ev[4 * p + 2], s));
     FK_TRY(sorted_expand(c, pl, nchunks, pk, c->st_keys[p], c->st_cb[p]));
