@@ -1730,10 +1730,21 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
-            if (nfb0)
+#ifndef FK_MID_WAVE
+#define FK_MID_WAVE 1  // A/B builds (-DFK_MID_WAVE=0): the block kernel for every block-tier bucket
+#endif
+            if (nfb0) {
+                // block-tier buckets of at most WAVE_MID_CAP keys: one wave each (no workgroup barriers);
+                // the block kernel takes the larger ones
+                if (FK_MID_WAVE)
+                    HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), fb0, nfb0, k,
+                                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                           B.bucket_unique->as<uint64_t>(), s, ordered));
                 HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nfb0, k, okb.as<uint64_t>(),
                                               B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                              c->misc.as<unsigned long long>() + 1, cap, 99, fb0, s));
+                                              c->misc.as<unsigned long long>() + 1, cap, 99, fb0, s,
+                                              FK_MID_WAVE ? WAVE_MID_CAP : 0u));
+            }
             if (nfb1) {
                 // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
                 HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfb1, k, okb.as<uint64_t>(),

@@ -188,11 +188,12 @@ hipError_t launch_bucket_write(const uint64_t *cell_base, const uint32_t *flags,
 hipError_t launch_bucket_count64(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                  uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                  unsigned long long *oversize, uint32_t small_limit, int dbg_phase,
-                                 const uint32_t *list, hipStream_t s);
+                                 const uint32_t *list, hipStream_t s, uint32_t skip_le = 0);
 hipError_t launch_bucket_count64_big(const BucketSrc &src, const Bucket *buckets, uint64_t nlist, int k,
                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                      unsigned long long *oversize, const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
+constexpr uint32_t WAVE_MID_CAP = 1024;  // 64-bit mid wave tier: listed buckets of 513 .. 1024 keys
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
@@ -221,6 +222,10 @@ hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave
 hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                       const uint32_t *list, hipStream_t s, bool ordered = true);
+// the listed block-tier buckets of at most WAVE_MID_CAP keys, one wave each (k <= 32)
+hipError_t launch_bucket_count64_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
+                                          uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
+                                          uint64_t *bucket_unique, hipStream_t s, bool ordered = true);
 // heavy buckets (above the wave tier, k <= 32) split into wave-sized sub-buckets by the key bits
 // below their common prefix (k_bucket_split64), counted by the wave tier (k_sub_count64_wave) and
 // joined back into the bucket's output region (k_bucket_join)
