@@ -336,7 +336,7 @@ def leg_line(args, topo: Topology, res: dict) -> dict:
         "pcie_h2d_GBps": res["fasta_bytes"] / (hs["ms_h2d"] * 1e-3) / 1e9 if hs["ms_h2d"] else None,
         "kmers_per_gpu": hs["kmers"], "distinct_rank0": hs["distinct"],
         "buckets_rank0": {"all": hs["buckets"], "above_wave_tier": hs["block_buckets"] + hs["big_buckets"],
-                          "above_2048_keys": hs["big_buckets"], "kmers_above_wave_tier": hs["heavy_keys"],
+                          "above_block_tier": hs["big_buckets"], "kmers_above_wave_tier": hs["heavy_keys"],
                           "split": hs["split_buckets"], "sub_buckets": hs["sub_buckets"],
                           "large_path": hs["oversize_buckets"], "cell_bits": hs["fine_bits"]},
     }

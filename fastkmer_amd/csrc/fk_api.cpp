@@ -1613,7 +1613,12 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     if (tiered) {
         FK_TRY(ensure(*B.tier_list, nbuckets * 8));
         uint32_t *lists = B.tier_list->as<uint32_t>();
-        HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, cap,
+#ifndef FK_SPLIT_HEAVY
+#define FK_SPLIT_HEAVY 1  // A/B builds (build_variant "nosplit", -DFK_SPLIT_HEAVY=0): no heavy-bucket split
+#endif
+        // the block tier's top: 64-bit keys with the split, the mid wave tier's cap (above it: split)
+        const uint32_t block_top = (c->KW == 1 && FK_SPLIT_HEAVY) ? WAVE_MID_CAP : cap;
+        HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, block_top,
                                     B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(),
                                     c->misc.as<unsigned long long>() + 3, s));
         // the tier sizes (and the listed buckets' keys) go to pinned memory right behind the tier
@@ -1640,24 +1645,18 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         c->stats.big_buckets = ntier[1];
         hipStream_t ts = s;
         uint64_t nlarge = 0;
-#ifndef FK_SPLIT_HEAVY
-#define FK_SPLIT_HEAVY 1  // A/B builds (build_variant "nosplit", -DFK_SPLIT_HEAVY=0): no heavy-bucket split
-#endif
         if (c->KW == 1 && (ntier[0] || ntier[1])) {
-            // 64-bit keys: the buckets above the block tier split into wave-sized sub-buckets by sampled
-            // splitters, counted by the wave tier and joined back; the buckets with a sub-bucket too
-            // large for a wave keep the big-table kernel.  The block tier (513..2048 keys) keeps its
-            // kernel: splitting it too measured the same at the configs[2] load and 0.35 ms slower at
-            // configs[1] (FK_SPLIT_BLOCK=1 builds it for A/B)
-#ifndef FK_SPLIT_BLOCK
-#define FK_SPLIT_BLOCK 0
-#endif
-            const uint32_t n0s = FK_SPLIT_BLOCK ? ntier[0] : 0u;
-            const uint32_t nl = n0s + ntier[1];
+            // 64-bit keys above the wave tier.  The block tier (513 .. WAVE_MID_CAP keys) is counted by
+            // the mid wave tier, one wave per bucket.  The big tier (above it) is split into wave-sized
+            // sub-buckets by sampled splitters, counted by the wave tier and joined back; a bucket with a
+            // sub-bucket too large for a wave (a k-mer repeated that often) falls back to the block
+            // kernel (<= cap keys) or the big-table kernel.  Without the split (-DFK_SPLIT_HEAVY=0, A/B
+            // builds) the block tier reaches cap and the block kernel takes its buckets above WAVE_MID_CAP.
             const uint32_t *l1 = lists + nbuckets;
-            uint32_t *fb0 = lists, *fb1 = lists + nbuckets;  // the fallbacks (no split: every listed bucket)
-            uint32_t nfb0 = ntier[0], nfb1 = ntier[1];
+            uint32_t *fbB = nullptr, *fbG = lists + nbuckets;  // the block / big-table kernels' lists
+            uint32_t nfbB = 0, nfbG = ntier[1];
             if (FK_SPLIT_HEAVY) {
+                const uint32_t nl = ntier[1];
                 const uint64_t maxsub = listed_keys / 64 + nl + 64;  // >= ceil(n / SPL_TGT) sub-buckets per bucket
                 FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
                 FK_TRY(ensure(c->sp_keys, listed_keys * 8));
@@ -1667,37 +1666,32 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
                 uint32_t *fb = c->sp_fb.as<uint32_t>();
                 unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
-                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, n0s, l1, ntier[1],
-                                            c->sp_base.as<uint64_t>(), s));
+                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(), s));
                 HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
                                           c->sp_base.as<uint64_t>() + nl, c->ws, s));
-                HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, n0s, l1, ntier[1],
-                                              c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
-                                              c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb, fb + nl,
-                                              cap, k, F, s));
+                HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(),
+                                              c->sp_keys.as<uint64_t>(), c->sp_subs.as<SubBucket>(),
+                                              c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, s));
                 HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipEventRecord(c->tier_ev, s));
                 HIP_TRY(hipEventSynchronize(c->tier_ev));
                 const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
                 const uint32_t nsub = sc[0];
-                if (n0s) nfb0 = sc[1], fb0 = fb;
-                nfb1 = sc[2], fb1 = fb + nl;
+                fbB = fb, nfbB = sc[1], fbG = fb + nl, nfbG = sc[2];
                 htrace("sorted: split counts read");
 #ifdef FK_PROBES
-                if (getenv("FASTKMER_HOST_TRACE")) {  // the listed buckets by size class: buckets, keys, fallbacks
+                if (getenv("FASTKMER_HOST_TRACE")) {  // the split buckets by size class: buckets, keys, fallbacks
                     std::vector<uint64_t> base((size_t)nl + 1);
-                    std::vector<uint32_t> f(2 * (size_t)nl);
+                    std::vector<uint32_t> f(2 * (size_t)nl), h_l((size_t)nl);
                     HIP_TRY(hipMemcpy(base.data(), c->sp_base.p, base.size() * 8, hipMemcpyDeviceToHost));
                     HIP_TRY(hipMemcpy(f.data(), fb, f.size() * 4, hipMemcpyDeviceToHost));
-                    std::vector<uint32_t> h_l((size_t)nl);
-                    HIP_TRY(hipMemcpy(h_l.data(), lists, (size_t)n0s * 4, hipMemcpyDeviceToHost));
-                    HIP_TRY(hipMemcpy(h_l.data() + n0s, l1, (size_t)ntier[1] * 4, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipMemcpy(h_l.data(), l1, (size_t)nl * 4, hipMemcpyDeviceToHost));
                     std::unordered_map<uint32_t, uint32_t> pos;
                     for (uint32_t j = 0; j < nl; ++j) pos[h_l[j]] = j;
                     uint64_t hb[40] = {}, hk[40] = {}, hf[40] = {}, hfk[40] = {};
                     std::vector<char> isfb(nl, 0);
                     for (uint32_t j = 0; j < sc[1]; ++j) isfb[pos[f[j]]] = 1;
-                    for (uint32_t j = 0; j < nfb1; ++j) isfb[pos[f[nl + j]]] = 1;
+                    for (uint32_t j = 0; j < sc[2]; ++j) isfb[pos[f[nl + j]]] = 1;
                     for (uint32_t j = 0; j < nl; ++j) {
                         const uint64_t n = base[j + 1] - base[j];
                         const int cl = 63 - __builtin_clzll(n | 1);
@@ -1709,8 +1703,8 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     HIP_TRY(rank_probe_read(rk, true));
                     fprintf(stderr, "probe_rank (wave tier, before the split): iterations %llu keys %llu buckets %llu "
                             "wall (small groups) %llu\n", rk[0], rk[1], rk[2], rk[3]);
-                    fprintf(stderr, "probe_split: listed %u keys %llu subs %u fallbacks %u + %u\n", nl,
-                            (unsigned long long)base[nl], nsub, sc[1], nfb1);
+                    fprintf(stderr, "probe_split: split %u keys %llu subs %u fallbacks %u + %u\n", nl,
+                            (unsigned long long)base[nl], nsub, sc[1], sc[2]);
                     for (int cl = 0; cl < 40; ++cl)
                         if (hb[cl])
                             fprintf(stderr, "probe_split: n in [2^%d, 2^%d): buckets %llu keys %llu fallback buckets %llu keys %llu\n",
@@ -1723,43 +1717,41 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
                                                 okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                                 c->sp_uniq.as<uint64_t>(), s, ordered));
-                HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, n0s, l1, ntier[1],
-                                           c->sp_par.as<SplitParent>(), c->sp_subs.as<SubBucket>(),
-                                           c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                           B.bucket_unique->as<uint64_t>(), s));
+                HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_par.as<SplitParent>(),
+                                           c->sp_subs.as<SubBucket>(), c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(),
+                                           B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(), s));
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
-#ifndef FK_MID_WAVE
-#define FK_MID_WAVE 1  // A/B builds (-DFK_MID_WAVE=0): the block kernel for every block-tier bucket
-#endif
-            if (nfb0) {
-                // block-tier buckets of at most WAVE_MID_CAP keys: one wave each (no workgroup barriers);
-                // the block kernel takes the larger ones
-                if (FK_MID_WAVE)
-                    HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), fb0, nfb0, k,
-                                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                           B.bucket_unique->as<uint64_t>(), s, ordered));
-                HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nfb0, k, okb.as<uint64_t>(),
-                                              B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                              c->misc.as<unsigned long long>() + 1, cap, 99, fb0, s,
-                                              FK_MID_WAVE ? WAVE_MID_CAP : 0u));
-            }
-            if (nfb1) {
-                // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
-                HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfb1, k, okb.as<uint64_t>(),
+            if (ntier[0]) {
+                HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                       B.bucket_unique->as<uint64_t>(), s, ordered));
+                if (block_top > WAVE_MID_CAP)  // no split: the block tier's buckets above the mid wave tier
+                    HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k, okb.as<uint64_t>(),
                                                   B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                  c->misc.as<unsigned long long>() + 2, fb1, s));
+                                                  c->misc.as<unsigned long long>() + 1, cap, 99, lists, s,
+                                                  WAVE_MID_CAP));
+            }
+            if (nfbB)
+                HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nfbB, k, okb.as<uint64_t>(),
+                                              B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                              c->misc.as<unsigned long long>() + 1, cap, 99, fbB, s));
+            if (nfbG) {
+                // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
+                HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfbG, k, okb.as<uint64_t>(),
+                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                                  c->misc.as<unsigned long long>() + 2, fbG, s));
                 HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
             }
             if (nlarge) {  // scratch for the listed buckets' keys only, taken by a cursor
                 FK_TRY(ensure(c->scratch, listed_keys * 8 * c->KW));
                 HIP_TRY(hipMemsetAsync(c->misc.as<unsigned long long>() + 6, 0, 8, s));
-                HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), nfb1, k,
+                HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), nfbG, k,
                                                  c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                 fb1, s, c->misc.as<unsigned long long>() + 6));
+                                                 fbG, s, c->misc.as<unsigned long long>() + 6));
             }
         } else if (ntier[0] || ntier[1]) {
             // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a

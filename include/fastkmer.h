@@ -86,8 +86,10 @@ typedef struct fk_stats {
     uint64_t pieces_counted;   /* staged pieces of the last fk_finish (0: one count of the whole input) */
     double ms_merge;           /* unused (0): staged pieces are counted once, never merged */
     uint64_t heavy_keys;       /* sorted count: k-mers in the buckets above the wave tier (split or block / big) */
-    uint64_t block_buckets;    /* buckets above the wave tier of at most 2048 keys (mid wave tier, block kernel) */
-    uint64_t big_buckets;      /* buckets above 2048 keys (the big-table kernel, then the large path) */
+    uint64_t block_buckets;    /* block tier: buckets above the wave tier of at most 1024 keys (k <= 32: the mid wave
+                                  tier) / 2048 keys (k > 32: mid wave tier, LDS sort) */
+    uint64_t big_buckets;      /* above the block tier (k <= 32: split into sub-buckets, fallbacks to the block /
+                                  big-table kernels; k > 32: the streaming path) */
     uint64_t ht_big_groups;    /* unused (0) */
     uint64_t split_buckets;    /* k <= 32: buckets above the wave tier split into wave-sized sub-buckets */
     uint64_t sub_buckets;      /* ... into this many sub-buckets (the wave tier counted them) */
