@@ -2924,7 +2924,8 @@ FK_EXPORT int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t
     const int KW = k <= 32 ? 1 : 2;
     const uint32_t cap = KW == 1 ? WAVE_BUCKET_CAP : WAVE128_BUCKET_CAP;
     if (n == 0 || n > cap) return set_err(FK_E_RANGE, "a wave bucket holds 1..%u keys", cap);
-    if (slots != (KW == 1 ? 768 : 384)) return set_err(FK_E_INVALID, "slots: 768 (k <= 32) or 384 (k > 32)");
+    if (slots != (int32_t)(KW == 1 ? WAVE_SLOTS : 384))
+        return set_err(FK_E_INVALID, "slots: %u (k <= 32) or 384 (k > 32)", WAVE_SLOTS);
     const int sh = 2 * k - F;
     for (uint32_t i = 0; i < n; ++i) {  // every key inside the bucket's cells
         const uint64_t hi = KW == 1 ? 0 : keys[2 * i], lo = KW == 1 ? keys[i] : keys[2 * i + 1];

@@ -193,6 +193,11 @@ hipError_t launch_bucket_count64_big(const BucketSrc &src, const Bucket *buckets
                                      uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                      unsigned long long *oversize, const uint32_t *list, hipStream_t s);
 constexpr uint32_t WAVE_BUCKET_CAP = 512;
+#ifndef FK_WAVE_SL
+#define FK_WAVE_SL 640  // table slots of a 512-key wave bucket (7.4 KB of LDS per wave, 6 waves per SIMD; 768:
+                        // 5, 1.4 ms slower at the configs[2] load, profiles/r05l_wave_slots_ab.txt)
+#endif
+constexpr uint32_t WAVE_SLOTS = FK_WAVE_SL;
 constexpr uint32_t WAVE_MID_CAP = 1024;  // 64-bit mid wave tier: listed buckets of 513 .. 1024 keys
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,

@@ -280,7 +280,7 @@ int fk_get_stats(fk_ctx *ctx, fk_stats *out);
  * One bucket through the wave-tier count kernel on `device`: the n keys
  * (k <= 32: one word each, n <= 512; 33 <= k <= 63: (hi, lo) pairs, n <= 256)
  * must lie in cells [c0, c1) of F cell bits (cell = top F bits of the 2k-bit
- * key); slots = table slots per bucket, the product's (768, or 384 for k > 32).
+ * key); slots = table slots per bucket, the product's (640, or 384 for k > 32).
  * Writes the distinct keys ascending and their counts, *n_out of them.  Lets
  * tests drive adversarial buckets (every key in one rank group, keys over all
  * groups) that FASTA inputs cannot aim at. */

@@ -2,7 +2,7 @@
 live in the dead table above CAP; FASTA inputs cannot aim at a bucket's groups).  Each bucket goes
 through fk_debug_wave_count (one bucket, one wave, the production kernel) and is compared with
 numpy's sorted unique counts: keys ascending, counts exact.  Covered for k = 31 (64-bit keys,
-512-key buckets, 768 slots) and k = 55 (128-bit keys, 256-key buckets, 384 slots):
+512-key buckets, 640 slots) and k = 55 (128-bit keys, 256-key buckets, 384 slots):
 U == CAP distinct keys in ONE rank group, keys over all groups, duplicates, the narrow (64 / 128
 group) and wide (256 group) ranks, multi-cell buckets."""
 import numpy as np
@@ -79,7 +79,7 @@ KINDS = ["one_group_full", "all_groups", "dups_one_group", "narrow_dups", "multi
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("slots", [768])
+@pytest.mark.parametrize("slots", [640])
 def test_wave64_adversarial_buckets(kind, slots):
     rng = np.random.default_rng(sum(kind.encode()) + slots)
     c0, c1 = (3, 9) if kind == "multi_cell" else (5, 6)
@@ -103,4 +103,4 @@ def test_wave128_adversarial_buckets(kind, slots):
 def test_wave_hook_rejects_keys_outside_the_cells():
     keys = np.array([np.uint64(7) << np.uint64(52)], dtype=np.uint64)
     with pytest.raises(fk.FastKmerError):
-        fk.debug_wave_count(keys, 31, F, 5, 6, 768)
+        fk.debug_wave_count(keys, 31, F, 5, 6, 640)
