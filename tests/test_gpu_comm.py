@@ -446,3 +446,62 @@ def test_split_of_another_rank_is_refused(tmp_path):
     assert e.value.code == -1
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_full_size_exchange_vs_one_count(world):
+    # BASELINE configs[1] (1 GB) through the in-process group at the product's own sizes (no piece
+    # knobs): each rank's one fk_ingest call sends ~10 steps of >= 128 MB while it ingests, the
+    # received segments are expanded on the staging stream as they land, the rest after the last
+    # step; the union of the ranks' bins must equal the same job counted whole from HBM (no
+    # communicator, no pieces) on all 2048 bins
+    import torch
+    n_reads = 1_000_000_000 // REC
+    dev = torch.empty(n_reads * REC, dtype=torch.uint8, device="cuda")
+    fk.synth_fasta_to_device(dev.data_ptr(), n_reads, 100, 100_000_000, seed=0x5EED + world)
+    host = torch.empty(dev.numel(), dtype=torch.uint8).pin_memory()
+    host.copy_(dev)
+    torch.cuda.synchronize()
+    ref = fk.KmerCounter(28, 10, 3, 2048)
+    ref.ingest_device(dev.data_ptr(), dev.numel())
+    ref.finish()
+    del dev
+    cuts = [r * n_reads // world * REC for r in range(world + 1)]
+    ctxs = [fk.KmerCounter(28, 10, 3, 2048, n_ranks=world, rank=r) for r in range(world)]
+    fk.comm_init_local(ctxs)
+    errs = [None] * world
+
+    def work(r):
+        try:
+            ctxs[r].ingest_ptr(host.data_ptr() + cuts[r], cuts[r + 1] - cuts[r])
+            ctxs[r].finish()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs[r] = e
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank did not finish"
+    for e in errs:
+        if e is not None:
+            raise e
+    sts = [c.stats() for c in ctxs]
+    # at least the ~10 steps of one rank's job (more with the closing steps)
+    assert all(st["xch_steps"] >= 8 for st in sts), [st["xch_steps"] for st in sts]
+    rst = ref.stats()
+    assert sum(st["kmers"] for st in sts) == rst["kmers"]
+    assert sum(st["distinct"] for st in sts) == rst["distinct"]
+    rsizes = ref.bin_sizes()
+    for r, c in enumerate(ctxs):
+        sizes = c.bin_sizes()
+        own = np.arange(2048) % world == r
+        assert np.all(sizes[~own] == 0) and np.array_equal(sizes[own], rsizes[own]), f"rank {r}"
+    for b in range(2048):
+        ka, ca = ctxs[b % world].get_bin(b)
+        kb, cb = ref.get_bin(b)
+        assert np.array_equal(ka, kb) and np.array_equal(ca, cb), f"bin {b}"
+    for c in ctxs:
+        c.close()
+    ref.close()
