@@ -199,6 +199,11 @@ constexpr uint32_t WAVE_BUCKET_CAP = 512;
 #endif
 constexpr uint32_t WAVE_SLOTS = FK_WAVE_SL;
 constexpr uint32_t WAVE_MID_CAP = 1024;  // 64-bit mid wave tier: listed buckets of 513 .. 1024 keys
+#ifndef FK_MID_SL
+#define FK_MID_SL 1280  // its table slots (14.6 KB per wave; 1536: kernel 2.15 vs 2.03 ms at the configs[2]
+                        // load, profiles/r05q_mid_slots_ab.txt)
+#endif
+constexpr uint32_t WAVE_MID_SLOTS = FK_MID_SL;
 constexpr uint32_t WAVE128_BUCKET_CAP = 256;  // keys per wave-tier bucket, 128-bit keys (k_bucket_count128_wave)
 hipError_t launch_bucket_count128_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                        uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
