@@ -846,8 +846,16 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     HIP_TRY(hipEventRecord(c->h2d_ev[0], cs));
     if (pinned) {
         // every segment's copy is queued first, so the DMA runs back to back even while the
-        // host waits on a piece's exchange
-        const size_t seg = c->ingest_seg, nseg = (n + seg - 1) / seg;
+        // host waits on a piece's exchange.  Each copy boundary costs ~11 us of link time
+        // (profiles/r05s_h2d_rates.txt): up to the call's last tenth (at least four small
+        // segments) the segments grow to a fiftieth of the call in whole ingest_segs, at most four (a
+        // 6.25 GB job: 128 MB; 1 GB: ingest_seg, whose pieces' cuts would move with larger segments,
+        // profiles/r05t_seg_ab.txt), ingest_seg in that last tenth, so that what follows the last
+        // byte (the last segment's map, the last piece) stays short
+        const size_t seg = c->ingest_seg, big = seg * std::clamp<size_t>((n / 50 + seg / 2) / seg, 1, 4),
+                     nseg = (n + seg - 1) / seg;
+        const size_t small_from = n - std::min(n, std::max<size_t>(n / 10, 4 * seg));
+        auto seg_len = [&](size_t off) { return std::min(off < small_from ? big : seg, n - off); };
         while (c->pm_active && c->seg_evs.size() < nseg) {
             hipEvent_t e = nullptr;
             HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -855,7 +863,7 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         }
         size_t off = 0;
         for (size_t i = 0; off < n; ++i) {
-            const size_t len = std::min(seg, n - off);
+            const size_t len = seg_len(off);
             HIP_TRY(hipMemcpyAsync(dst + off, fasta + off, len, hipMemcpyHostToDevice, cs));
             if (c->pm_active) HIP_TRY(hipEventRecord(c->seg_evs[i], cs));
             off += len;
@@ -863,7 +871,7 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
         off = 0;
         for (size_t i = 0; c->pm_active && off < n; ++i) {
-            off += std::min(seg, n - off);
+            off += seg_len(off);
             HIP_TRY(hipStreamWaitEvent(s, c->seg_evs[i], 0));
             FK_TRY(premap_launch(c, have + off, last && off == n));
             if (pieces) FK_TRY(xch_maybe_piece(c));
