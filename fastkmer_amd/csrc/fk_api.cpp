@@ -330,6 +330,8 @@ struct fk_ctx {
     double ms_h2d = 0.0;  // last fk_ingest: first copy issued -> last copy done
     bool ev_parse = false, ev_sig = false, ev_part = false, ev_count = false;
     std::vector<hipEvent_t> seg_evs;  // fk_ingest, pinned source: one "segment landed" event per segment
+    std::vector<hipEvent_t> map_evs;  // ... and one "segment mapped" event (one rank's staged pieces)
+    std::vector<uint64_t> seg_tiles;  // ... the tiles mapped once that segment's map is done
     PinBuf pin_up, pin_down;              // staging: chunk tables up, per-bin counts down
     PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
@@ -566,6 +568,10 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->own_stream = true;
     e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->seg_ev, hipEventDisableTiming);
+    // staged pieces are partitioned and expanded on their own stream (one rank: so that the map of
+    // later segments never queues behind a piece's expansion; the exchange: the received segments)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xstage, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xstage_ev, hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreate(&c->h2d_ev[i]);
     if (e != hipSuccess) {
         fk_destroy(c);
@@ -626,6 +632,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     for (auto &e : c->xev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : c->seg_evs)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : c->map_evs)
         if (e) (void)hipEventDestroy(e);
     if (c->emit_ev) (void)hipEventDestroy(c->emit_ev);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -747,7 +755,7 @@ static int premap_launch(fk_ctx *c, uint64_t landed, bool final_) {
 }
 
 static int xch_maybe_piece(fk_ctx *c);
-static int local_maybe_piece(fk_ctx *c);
+static int local_maybe_piece(fk_ctx *c, uint64_t tiles, hipEvent_t mapped);
 static void xch_reset(fk_ctx *c);
 static void pieces_reset(fk_ctx *c);
 
@@ -779,9 +787,9 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         if (c->comm) {
             if (c->xch.open) return set_err(FK_E_STATE, "fk_ingest: the previous job's exchange is unfinished (fk_finish)");
             HIP_TRY(hipStreamSynchronize(c->comm_stream));
-            HIP_TRY(hipStreamSynchronize(c->xstage));
             xch_reset(c);
         }
+        HIP_TRY(hipStreamSynchronize(c->xstage));
         HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
         pieces_reset(c);
         c->pm_active = premap_eligible(c);
@@ -869,14 +877,29 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
             off += len;
         }
         HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
+        // every segment's map is queued too (one rank; the exchange steps wait on the host between
+        // them), then the pieces are staged on the staging stream behind the map of their last
+        // segment: the host's waits for a piece's partition never hold back a later map launch
+        while (!pieces && c->pm_active && c->map_evs.size() < nseg) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->map_evs.push_back(e);
+        }
+        c->seg_tiles.clear();
         off = 0;
         for (size_t i = 0; c->pm_active && off < n; ++i) {
             off += seg_len(off);
             HIP_TRY(hipStreamWaitEvent(s, c->seg_evs[i], 0));
             FK_TRY(premap_launch(c, have + off, last && off == n));
-            if (pieces) FK_TRY(xch_maybe_piece(c));
-            else if (c->pm_active) FK_TRY(local_maybe_piece(c));
+            if (pieces) {
+                FK_TRY(xch_maybe_piece(c));
+            } else {
+                HIP_TRY(hipEventRecord(c->map_evs[i], s));
+                c->seg_tiles.push_back(c->pm_tiles);
+            }
         }
+        for (size_t i = 0; !pieces && c->pm_active && i < c->seg_tiles.size(); ++i)
+            FK_TRY(local_maybe_piece(c, c->seg_tiles[i], c->map_evs[i]));
     } else {
         size_t off = 0;
         for (int i = 0; off < n; ++i) {
@@ -890,8 +913,12 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
                 HIP_TRY(hipEventRecord(c->seg_ev, cs));
                 HIP_TRY(hipStreamWaitEvent(s, c->seg_ev, 0));
                 FK_TRY(premap_launch(c, have + off, last && off == n));
-                if (pieces) FK_TRY(xch_maybe_piece(c));
-                else FK_TRY(local_maybe_piece(c));
+                if (pieces) {
+                    FK_TRY(xch_maybe_piece(c));
+                } else {
+                    HIP_TRY(hipEventRecord(c->seg_ev, s));  // reused: the staging stream waits on it at once
+                    FK_TRY(local_maybe_piece(c, c->pm_tiles, c->seg_ev));
+                }
             }
         }
         HIP_TRY(hipEventRecord(c->h2d_ev[1], cs));
@@ -1315,6 +1342,8 @@ static int build_group_table(fk_ctx *c);
 FK_EXPORT int fk_map(fk_ctx *c, uint64_t *send_counts) {
     if (!c) return set_err(FK_E_INVALID, "null ctx");
     DeviceGuard dg_(c->device);
+    // one rank: the pieces staged during fk_ingest read the mapped tiles on the staging stream
+    if (c->st_np && !c->comm) HIP_TRY(hipStreamWaitEvent(c->stream, c->xstage_ev, 0));
     FK_TRY(map_records(c));
     const double t_start = now_ms();
     hipStream_t s = c->stream;
@@ -2213,32 +2242,53 @@ static int staged_count(fk_ctx *c) {
 // FASTKMER_PIECE_BYTES, at the fractions st_cuts of it (the last piece -- expanded after the last byte
 // lands -- is the smallest); jobs under 2 * MIN_PIECE are counted whole.  A streamed job of unknown
 // size: every piece_bytes.  At most STAGE_MAXP - 1 pieces before fk_finish stages the last one.
-static bool local_piece_due(const fk_ctx *c) {
+static bool local_piece_due(const fk_ctx *c, uint64_t tiles) {
     constexpr uint64_t MIN_PIECE = 256ull << 20;
     if (c->st_np >= (uint32_t)STAGE_MAXP - 1) return false;
     const uint64_t tile = fm_tile_bytes(FUSED_NT);
     if (c->job_bytes && !c->piece_bytes_set) {
         if (c->job_bytes < 2 * MIN_PIECE || c->st_cut >= c->st_cuts.size()) return false;
         const uint64_t end = (uint64_t)(c->st_cuts[c->st_cut] * (double)c->job_bytes);
-        return c->pm_tiles * tile >= end && (c->pm_tiles - c->tiles_counted) * tile >= MIN_PIECE / 2;
+        return tiles * tile >= end && (tiles - c->tiles_counted) * tile >= MIN_PIECE / 2;
     }
-    return (c->pm_tiles - c->tiles_counted) * tile >= c->piece_bytes;
+    return (tiles - c->tiles_counted) * tile >= c->piece_bytes;
 }
 
-static int local_maybe_piece(fk_ctx *c) {
-    if (!staged_eligible(c) || c->pieces_void || !local_piece_due(c)) return FK_OK;
+// The context's stream and scan workspace swapped for the staging stream's while a staging step is
+// queued (the expansion code queues on c->stream).
+struct StageStream {
+    fk_ctx *c;
+    explicit StageStream(fk_ctx *c_) : c(c_) {
+        std::swap(c->stream, c->xstage);
+        std::swap(c->ws, c->ws_x);
+    }
+    ~StageStream() {
+        std::swap(c->stream, c->xstage);
+        std::swap(c->ws, c->ws_x);
+    }
+};
+
+// tiles: the tiles mapped once `mapped` (recorded on the map stream) has passed.  The piece is
+// partitioned and expanded on the staging stream (StageStream), which fk_finish joins (xstage_ev).
+static int local_maybe_piece(fk_ctx *c, uint64_t tiles, hipEvent_t mapped) {
+    if (!staged_eligible(c) || c->pieces_void || !local_piece_due(c, tiles)) return FK_OK;
+    StageStream ss_(c);
+    hipStream_t s = c->stream;  // the staging stream
+    HIP_TRY(hipStreamWaitEvent(s, mapped, 0));
     uint64_t h[4] = {0, 0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     if (h[2]) {
         c->pieces_void = true;
         return FK_OK;
     }
-    const uint64_t t0 = c->tiles_counted, nt = c->pm_tiles - t0;
+    const uint64_t t0 = c->tiles_counted, nt = tiles - t0;
     const RecSrc src = fused_src(c, t0, nt, nt * map_fused_tcap());
-    c->tiles_counted = c->pm_tiles;
+    c->tiles_counted = tiles;
     c->st_cut += 1;
-    return staged_expand(c, src, c->job_bytes ? (double)(nt * fm_tile_bytes(FUSED_NT)) / (double)c->job_bytes : 0.0);
+    FK_TRY(staged_expand(c, src, c->job_bytes ? (double)(nt * fm_tile_bytes(FUSED_NT)) / (double)c->job_bytes : 0.0));
+    HIP_TRY(hipEventRecord(c->xstage_ev, s));
+    return FK_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -2464,20 +2514,6 @@ static int segment_ranges(fk_ctx *c, size_t s0, size_t s1, std::vector<std::vect
 // With a communicator and staged pieces: expands the received segments [segs_counted, s1) as one
 // staged piece (they arrive grouped by local bin: no partition), once the comm stream has
 // delivered them.  `frac` = their estimated fraction of what this rank receives in the job.
-// The context's stream and scan workspace swapped for the staging stream's while a staging step is
-// queued (the expansion code queues on c->stream).
-struct StageStream {
-    fk_ctx *c;
-    explicit StageStream(fk_ctx *c_) : c(c_) {
-        std::swap(c->stream, c->xstage);
-        std::swap(c->ws, c->ws_x);
-    }
-    ~StageStream() {
-        std::swap(c->stream, c->xstage);
-        std::swap(c->ws, c->ws_x);
-    }
-};
-
 static int xch_stage_segments(fk_ctx *c, size_t s1, double frac) {
     if (s1 <= c->segs_counted) return FK_OK;
     const uint32_t p = c->st_np;
@@ -2633,7 +2669,7 @@ static int finish_local(fk_ctx *c) {
     if (c->G != 1)
         return set_err(FK_E_STATE, "fk_finish over %u ranks needs a communicator (fk_comm_init); or use "
                                    "fk_map/fk_map_emit/fk_reduce", c->G);
-    FK_TRY(fk_map(c, nullptr));
+    FK_TRY(fk_map(c, nullptr));  // joins the staging stream first
     DeviceGuard dg_(c->device);
     if (c->st_np && c->rec_tiled && !c->pieces_void && c->tiles_counted <= c->rec_tiles) {
         // staged pieces were expanded while the input landed: the last piece, then one count

@@ -44,7 +44,11 @@ struct Bucket {
 // the staged pieces' key arrays (one job's input expanded piece by piece while it landed, and
 // counted once): piece p holds the bucket's keys at pk[p][pcb[p][g0] .. pcb[p][g1]), g0 / g1 =
 // (lbin << F) + c0 / c1, pcb[p] the exclusive scan of the piece's cell totals.
-constexpr int STAGE_MAXP = 4;
+#ifndef FK_STAGE_MAXP
+#define FK_STAGE_MAXP 4
+#endif
+constexpr int STAGE_MAXP = FK_STAGE_MAXP;
+static_assert(STAGE_MAXP >= 2 && STAGE_MAXP <= 8, "staged pieces per job");
 struct BucketSrc {
     const uint64_t *keys;
     int F;  // cell bits: a bucket's keys lie in [c0 << (2k-F), c1 << (2k-F))
