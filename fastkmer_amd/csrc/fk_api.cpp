@@ -318,7 +318,7 @@ struct fk_ctx {
     DevBuf chunk_nk, chunk_base, lp, cell_total, cell_base, flags, flag_scan, buckets, keys, out_keys, out_counts;
     DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_total;
-    DevBuf sp_base, sp_keys, sp_subs, sp_par, sp_uniq, sp_fb;  // heavy buckets split into sub-buckets
+    DevBuf sp_base, sp_keys, sp_subs, sp_par, sp_fb;  // heavy buckets split into sub-buckets
     ScanWorkspace ws;
     // results
     bool have_result = false;
@@ -612,7 +612,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts,
-                      &c->sp_base, &c->sp_keys, &c->sp_subs, &c->sp_par, &c->sp_uniq, &c->sp_fb};
+                      &c->sp_base, &c->sp_keys, &c->sp_subs, &c->sp_par, &c->sp_fb};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -1699,7 +1699,6 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 FK_TRY(ensure(c->sp_keys, listed_keys * 8));
                 FK_TRY(ensure(c->sp_subs, maxsub * sizeof(SubBucket)));
                 FK_TRY(ensure(c->sp_par, (uint64_t)nl * sizeof(SplitParent)));
-                FK_TRY(ensure(c->sp_uniq, maxsub * 8));
                 FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
                 uint32_t *fb = c->sp_fb.as<uint32_t>();
                 unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
@@ -1751,12 +1750,10 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
 #endif
                 if (nsub > maxsub) return set_err(FK_E_DEVICE, "bucket split: %u sub-buckets of at most %llu", nsub,
                                                   (unsigned long long)maxsub);
-                HIP_TRY(launch_sub_count64_wave(c->sp_subs.as<SubBucket>(), nsub, c->sp_keys.as<uint64_t>(),
-                                                okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                c->sp_uniq.as<uint64_t>(), s, ordered));
-                HIP_TRY(launch_bucket_join(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_par.as<SplitParent>(),
-                                           c->sp_subs.as<SubBucket>(), c->sp_uniq.as<uint64_t>(), okb.as<uint64_t>(),
-                                           B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(), s));
+                HIP_TRY(launch_sub_count64_seq(B.buckets->as<Bucket>(), l1, nl, c->sp_par.as<SplitParent>(),
+                                               c->sp_subs.as<SubBucket>(), c->sp_keys.as<uint64_t>(), okb.as<uint64_t>(),
+                                               B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(), s,
+                                               ordered));
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
@@ -2358,7 +2355,7 @@ static int note_held(fk_ctx *c, int rc) {
     FK_HELD(scratch); FK_HELD(keys); FK_HELD(out_keys); FK_HELD(out_counts); FK_HELD(buckets);
     FK_HELD(flags); FK_HELD(flag_scan); FK_HELD(cell_total); FK_HELD(cell_base); FK_HELD(dense_keys);
     FK_HELD(dense_counts); FK_HELD(bucket_unique);
-    FK_HELD(sp_keys); FK_HELD(sp_subs); FK_HELD(sp_uniq); FK_HELD(xsend); FK_HELD(xrecv);
+    FK_HELD(sp_keys); FK_HELD(sp_subs); FK_HELD(xsend); FK_HELD(xrecv);
     FK_HELD(gather_keys); FK_HELD(st_keys[0]); FK_HELD(st_keys[1]); FK_HELD(st_keys[2]); FK_HELD(st_keys[3]);
     FK_HELD(part.K); FK_HELD(part.KT); FK_HELD(dest.K); FK_HELD(dest.KT);
 #undef FK_HELD

@@ -240,12 +240,10 @@ hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *bucket
 hipError_t launch_bucket_count64_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
                                           uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
                                           uint64_t *bucket_unique, hipStream_t s, bool ordered = true);
-// heavy buckets (above the wave tier, k <= 32) split into wave-sized sub-buckets by the key bits
-// below their common prefix (k_bucket_split64), counted by the wave tier (k_sub_count64_wave) and
-// joined back into the bucket's output region (k_bucket_join)
+// heavy buckets (above the wave tier, k <= 32) split into wave-sized sub-buckets by sampled
+// splitters (k_bucket_split64), counted in order by one wave per bucket (k_sub_count64_seq)
 struct SubBucket {
     uint64_t src;   // first key in the split copy (skeys)
-    uint64_t out;   // first output slot (the parent bucket's region of out_keys / out_counts)
     uint64_t lo;    // every key lies in [lo, lo + 2^span) (the rank's group cut)
     uint32_t n, span;
 };
@@ -261,12 +259,9 @@ hipError_t launch_bucket_split64(const BucketSrc &src, const Bucket *buckets, co
                                  const uint32_t *list1, uint32_t n1, const uint64_t *sbase, uint64_t *skeys,
                                  SubBucket *subs, SplitParent *parents, unsigned int *counts, uint32_t *fb0,
                                  uint32_t *fb1, uint32_t block_cap, int k, int F, hipStream_t s);
-hipError_t launch_sub_count64_wave(const SubBucket *subs, uint64_t nsubs, const uint64_t *skeys, uint64_t *out_keys,
-                                   uint32_t *out_counts, uint64_t *sub_unique, hipStream_t s, bool ordered = true);
-hipError_t launch_bucket_join(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
-                              uint32_t n1, const SplitParent *parents, const SubBucket *subs,
-                              const uint64_t *sub_unique, uint64_t *out_keys, uint32_t *out_counts,
-                              uint64_t *bucket_unique, hipStream_t s);
+hipError_t launch_sub_count64_seq(const Bucket *buckets, const uint32_t *list, uint32_t nl, const SplitParent *parents,
+                                  const SubBucket *subs, const uint64_t *skeys, uint64_t *out_keys,
+                                  uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s, bool ordered);
 // dst[i] += src[i] (dst = src when `copy`)
 hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
 // skip_le: listed buckets of at most this many keys were counted by a wave tier (skipped)
