@@ -860,7 +860,10 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         // 6.25 GB job: 128 MB; 1 GB: ingest_seg, whose pieces' cuts would move with larger segments,
         // profiles/r05t_seg_ab.txt), ingest_seg in that last tenth, so that what follows the last
         // byte (the last segment's map, the last piece) stays short
-        const size_t seg = c->ingest_seg, big = seg * std::clamp<size_t>((n / 50 + seg / 2) / seg, 1, 4),
+        #ifndef FK_SEG_DIV
+#define FK_SEG_DIV 50  // A/B builds: -DFK_SEG_DIV=16 (1 GB: 64 MB segments)
+#endif
+        const size_t seg = c->ingest_seg, big = seg * std::clamp<size_t>((n / FK_SEG_DIV + seg / 2) / seg, 1, 4),
                      nseg = (n + seg - 1) / seg;
         const size_t small_from = n - std::min(n, std::max<size_t>(n / 10, 4 * seg));
         auto seg_len = [&](size_t off) { return std::min(off < small_from ? big : seg, n - off); };
