@@ -362,6 +362,10 @@ struct fk_ctx {
     uint64_t reserve_bytes = 0;   // fk_ingest_reserve's size for the next job
     size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) staged
     std::vector<double> st_cuts{0.4, 0.7, 0.9};  // piece ends of a staged job (FASTKMER_PIECE_CUTS; 45 / 70 / 85 % measured 22.84 vs 22.77 ms)
+    // ... with a communicator: earlier, a received piece lands a step's partition and transfer later
+    // (one in-process rank at the configs[2] load: 153.2-153.7 ms against 156.1-159.4 with the local
+    // cuts, profiles/r05z_xch_cuts_seg_ab.txt)
+    std::vector<double> xst_cuts{0.35, 0.65, 0.84};
     uint32_t st_np = 0;                          // pieces expanded in the current job
     uint32_t st_cut = 0;                         // one rank: st_cuts passed in the current job
     SortedPlan st_plan;                          // the job's cells (fixed by its first piece)
@@ -524,11 +528,12 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     }
     if (const char *v = env("FASTKMER_PIECE_CUTS")) {  // staged piece ends as job fractions, e.g. "0.4,0.7,0.9"
         c->st_cuts.clear();
+        c->xst_cuts.clear();
         for (const char *q = v; *q;) {
             char *e = nullptr;
             const double f = strtod(q, &e);
             if (e == q) break;
-            if (f > 0.0 && f < 1.0 && c->st_cuts.size() < STAGE_MAXP - 1) c->st_cuts.push_back(f);
+            if (f > 0.0 && f < 1.0 && c->st_cuts.size() < STAGE_MAXP - 1) c->st_cuts.push_back(f), c->xst_cuts.push_back(f);
             q = *e == ',' ? e + 1 : e;
         }
     }
@@ -856,15 +861,14 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         // every segment's copy is queued first, so the DMA runs back to back even while the
         // host waits on a piece's exchange.  Each copy boundary costs ~11 us of link time
         // (profiles/r05s_h2d_rates.txt): up to the call's last tenth (at least four small
-        // segments) the segments grow to a fiftieth of the call in whole ingest_segs, at most four (a
-        // 6.25 GB job: 128 MB; 1 GB: ingest_seg, whose pieces' cuts would move with larger segments,
-        // profiles/r05t_seg_ab.txt), ingest_seg in that last tenth, so that what follows the last
-        // byte (the last segment's map, the last piece) stays short
-        #ifndef FK_SEG_DIV
-#define FK_SEG_DIV 50  // A/B builds: -DFK_SEG_DIV=16 (1 GB: 64 MB segments)
-#endif
-        const size_t seg = c->ingest_seg, big = seg * std::clamp<size_t>((n / FK_SEG_DIV + seg / 2) / seg, 1, 4),
-                     nseg = (n + seg - 1) / seg;
+        // segments) the segments grow to a sixteenth of the call in whole ingest_segs, at most four
+        // (1 GB: 64 MB, 6.25 GB: 128 MB; configs[1] 22.70 -> 22.56 ms, profiles/r05z_xch_cuts_seg_ab.txt),
+        // with a communicator at most a quarter of an exchange step; ingest_seg in that last tenth, so
+        // that what follows the last byte (the last segment's map, the last piece) stays short
+        const size_t seg = c->ingest_seg;
+        size_t big = seg * std::clamp<size_t>((n / 16 + seg / 2) / seg, 1, 4);
+        if (pieces) big = std::min(big, std::max(seg, (size_t)c->piece_bytes / 4 / seg * seg));
+        const size_t nseg = (n + seg - 1) / seg;
         const size_t small_from = n - std::min(n, std::max<size_t>(n / 10, 4 * seg));
         auto seg_len = [&](size_t off) { return std::min(off < small_from ? big : seg, n - off); };
         while (c->pm_active && c->seg_evs.size() < nseg) {
@@ -2561,8 +2565,8 @@ static int xch_maybe_stage(fk_ctx *c, size_t s1) {
     // every quarter left ~30 % of a 6.25 GB rank for fk_finish: 61.7 ms after it against 47.7 for
     // the local path, profiles/r04c_xch_tail.txt.)
     if (frac > 0.0) {
-        if (c->st_np >= (uint32_t)c->st_cuts.size()) return FK_OK;
-        if (xch_recv_frac(c, before + recs) < c->st_cuts[c->st_np]) return FK_OK;
+        if (c->st_np >= (uint32_t)c->xst_cuts.size()) return FK_OK;
+        if (xch_recv_frac(c, before + recs) < c->xst_cuts[c->st_np]) return FK_OK;
     }
     return xch_stage_segments(c, s1, frac);
 }
