@@ -1642,11 +1642,12 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     HIP_TRY(launch_bucket_write(cell_base, B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), c->nlb, F, nbuckets,
                                 total_kmers, B.buckets->as<Bucket>(), s));
     BucketSrc src = src_in;
-    if (src.np > 0) {  // the staged pieces' starts per bucket, read by the wave tier
-        FK_TRY(ensure(*B.piece_starts, nbuckets * sizeof(PieceStarts)));
-        HIP_TRY(launch_bucket_pieces(src, B.buckets->as<Bucket>(), nbuckets, B.piece_starts->as<PieceStarts>(), s));
-        src.starts = B.piece_starts->as<PieceStarts>();
-    }
+    src.F = F;
+    if (src.np > 0) FK_TRY(ensure(*B.piece_starts, nbuckets * sizeof(PieceStarts)));
+    // the buckets' sizes, and the staged pieces' starts per bucket (read by the wave tier)
+    HIP_TRY(launch_bucket_finish(src, B.buckets->as<Bucket>(), nbuckets, c->nlb, total_kmers,
+                                 src.np > 0 ? B.piece_starts->as<PieceStarts>() : nullptr, s));
+    if (src.np > 0) src.starts = B.piece_starts->as<PieceStarts>();
     // 5: exact count per bucket in LDS; buckets that do not fit take the streaming path
     const uint32_t small_limit = c->force_large ? 0u : cap;
     HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));

@@ -55,7 +55,7 @@ struct BucketSrc {
     int np = 0;
     const uint64_t *pk[STAGE_MAXP] = {};
     const uint64_t *pcb[STAGE_MAXP] = {};
-    const struct PieceStarts *starts = nullptr;  // per bucket (launch_bucket_pieces), or null
+    const struct PieceStarts *starts = nullptr;  // per bucket (launch_bucket_finish), or null
 };
 // one bucket's keys in the staged pieces: piece p's first key at s[p] of pk[p], pre[p] keys of
 // the bucket in the pieces before p (pre[p] = ~0u for p >= np)
@@ -63,8 +63,9 @@ struct PieceStarts {
     uint64_t s[STAGE_MAXP];
     uint32_t pre[STAGE_MAXP];
 };
-hipError_t launch_bucket_pieces(const BucketSrc &src, const struct Bucket *buckets, uint64_t nb, PieceStarts *out,
-                                hipStream_t s);
+// every bucket's n / c1 (from the next bucket) and, with staged pieces (src.np > 0), its piece starts
+hipError_t launch_bucket_finish(const BucketSrc &src, struct Bucket *buckets, uint64_t nb, uint32_t nlbins,
+                                uint64_t total_keys, PieceStarts *out, hipStream_t s);
 
 struct Chunk {
     uint64_t rec_begin, rec_end;  // records [begin, end) of one local bin
