@@ -210,6 +210,42 @@ def exchange_figures(st: dict, world: int) -> dict:
 
 
 
+def pin_to_gpu_numa(local_rank: int):
+    """Best effort, before any GPU call: restrict this rank's CPUs to the NUMA node of its GPU (KFD
+    topology -> PCI address -> numa_node), so that its pinned host buffers -- first touched here --
+    sit next to the GPU's PCIe link.  Returns the node, or None (no sysfs, a visibility mask that
+    renumbers the devices, or any error: the affinity is left alone)."""
+    if any(os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")):
+        return None
+    try:
+        base = "/sys/class/kfd/kfd/topology/nodes"
+        gpus = []
+        for d in sorted(os.listdir(base), key=int):
+            with open(f"{base}/{d}/properties") as f:
+                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            if int(props.get("simd_count", "0")) > 0:
+                gpus.append(props)
+        p = gpus[local_rank]
+        loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7}"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read())
+        if node < 0:
+            return None
+        cpus = set()
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                cpus.update(range(int(lo), int(hi or lo) + 1))
+        cur = os.sched_getaffinity(0)
+        want = cur & cpus
+        if want and want != cur:
+            os.sched_setaffinity(0, want)
+        return node
+    except Exception:  # noqa: BLE001 -- best effort
+        return None
+
+
 class Topology:
     """Where this process sits: one rank of a torch.distributed job (one process per GPU, RCCL
     between them), the only rank, or --rehearse-local N ranks as threads on GPU 0."""
@@ -467,6 +503,7 @@ def main() -> None:
     # would hold both legs' buffers on its GPU at once (k = 55: ~57 GB per k-mer array)
     device_leg = not args.no_device_leg and (args.device_leg or (topo.n_ranks == 1 and nbytes <= 2_000_000_000))
     c3_leg = args.c3_leg == "on" or (args.c3_leg == "auto" and wl != "c3" and not topo.local)
+    numa = pin_to_gpu_numa(topo.local_rank) if topo.distributed else None
     torch.cuda.set_device(0 if topo.local else topo.local_rank)
     if topo.distributed:
         dist.init_process_group("gloo")  # bootstrap + host barriers; the records move over RCCL in the library
@@ -515,6 +552,8 @@ def main() -> None:
             out["roofline"] = roofline(args, topo, res)
         if res3 is not None:
             out["configs2_per_gpu"] = leg_line(args, topo, res3)
+        if topo.distributed:
+            out["numa_node_rank0"] = numa  # the node rank 0's CPUs were restricted to (None: left alone)
         if topo.n_ranks == 1 and not args.no_cpu_baseline and wl == "c2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_bytes, k, m, B, read_len, genome)
         print(json.dumps(out), flush=True)
