@@ -841,15 +841,19 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
     // the job's size: this call's when it holds the whole input, else what fk_ingest_reserve announced
     if (pieces && fresh) {
         c->xch.expect_bytes = last ? n : c->reserve_bytes;
-        // a job of known size goes out in about XCH_STEPS steps (at most 1 GB, at least 128 MB each):
+        // a job of known size goes out in about XCH_STEPS steps (at most 1 GB, at least XCH_MIN each):
         // every step but the last moves while later bytes are copied in (one 1 GB step for a 1 GB job
         // would leave the whole exchange after the last byte), and the staging cuts (st_cuts) fall on
         // step ends (1 GB steps of a 6.25 GB job staged 5-6 GB after the last byte: 11 ms of expansion
         // in the tail, profiles/r05d_xch1_c3_tail.txt)
         constexpr uint64_t XCH_STEPS = 10;
+#ifndef FK_XCH_MIN_MB
+#define FK_XCH_MIN_MB 64  // 1 GB job: ten steps (A/B builds: 128, seven steps)
+#endif
+        constexpr uint64_t XCH_MIN = (uint64_t)FK_XCH_MIN_MB << 20;
         if (!c->piece_bytes_set)
             c->piece_bytes = c->xch.expect_bytes
-                                 ? std::min<uint64_t>(1ull << 30, std::max<uint64_t>(128ull << 20, c->xch.expect_bytes / XCH_STEPS))
+                                 ? std::min<uint64_t>(1ull << 30, std::max<uint64_t>(XCH_MIN, c->xch.expect_bytes / XCH_STEPS))
                                  : 1ull << 30;
     }
     if (fresh) {

@@ -451,7 +451,7 @@ def test_split_of_another_rank_is_refused(tmp_path):
 @pytest.mark.parametrize("world", [1, 2])
 def test_full_size_exchange_vs_one_count(world):
     # BASELINE configs[1] (1 GB) through the in-process group at the product's own sizes (no piece
-    # knobs): each rank's one fk_ingest call sends steps of a tenth of its share (>= 128 MB) while
+    # knobs): each rank's one fk_ingest call sends steps of a tenth of its share (>= 64 MB) while
     # it ingests, the received segments are expanded on the staging stream as they land, the rest
     # after the last step; the union of the ranks' bins must equal the same job counted whole from HBM (no
     # communicator, no pieces) on all 2048 bins
@@ -488,8 +488,8 @@ def test_full_size_exchange_vs_one_count(world):
         if e is not None:
             raise e
     sts = [c.stats() for c in ctxs]
-    # a tenth of the rank's share per step, at least 128 MB: 7 steps for one rank, 4 for two
-    assert all(st["xch_steps"] >= (cuts[r + 1] - cuts[r]) // (128 << 20) for r, st in enumerate(sts)), \
+    # a tenth of the rank's share per step, at least 64 MB: 10 steps for one rank, 7 for two
+    assert all(st["xch_steps"] >= (cuts[r + 1] - cuts[r]) // (128 << 20) + 2 for r, st in enumerate(sts)), \
         [st["xch_steps"] for st in sts]
     rst = ref.stats()
     assert sum(st["kmers"] for st in sts) == rst["kmers"]
