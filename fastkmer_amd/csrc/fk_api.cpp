@@ -1666,6 +1666,8 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
 #define FK_SPLIT_HEAVY 1  // A/B builds (build_variant "nosplit", -DFK_SPLIT_HEAVY=0): no heavy-bucket split
 #endif
         // the block tier's top: 64-bit keys with the split, the mid wave tier's cap (above it: split)
+        // (the 513..1024-key buckets through the split as well, no mid wave tier: configs[2] load
+        // 1.1-1.4 ms slower, configs[1] 0.3 ms, profiles/r05zg_mid_split_ab.txt)
         const uint32_t block_top = (c->KW == 1 && FK_SPLIT_HEAVY) ? WAVE_MID_CAP : cap;
         HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, block_top,
                                     B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(),
