@@ -210,22 +210,50 @@ def exchange_figures(st: dict, world: int) -> dict:
 
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+VISIBILITY_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def kfd_gpus(root: str | None = None) -> list[dict]:
+    """The GPU nodes of the KFD topology (sysfs; properties with simd_count > 0), in node order.
+    Reading sysfs initialises nothing: the launcher counts GPUs this way, never through HIP."""
+    root = root or os.environ.get("FASTKMER_KFD_TOPOLOGY", KFD_TOPOLOGY)
+    gpus = []
+    try:
+        nodes = sorted((d for d in os.listdir(root) if d.isdigit()), key=int)
+    except OSError:
+        return gpus
+    for d in nodes:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            gpus.append(props)
+    return gpus
+
+
+def count_gpus(root: str | None = None) -> int:
+    """GPUs this process may use: the KFD topology's GPU nodes, narrowed by a visibility mask
+    (HIP_/ROCR_/CUDA_VISIBLE_DEVICES: its entries, at most the nodes present)."""
+    n = len(kfd_gpus(root))
+    for var in VISIBILITY_VARS:
+        v = os.environ.get(var)
+        if v:  # unset or empty: no mask
+            n = min(n, len([e for e in v.split(",") if e.strip()]))
+    return n
+
+
 def pin_to_gpu_numa(local_rank: int):
     """Best effort, before any GPU call: restrict this rank's CPUs to the NUMA node of its GPU (KFD
     topology -> PCI address -> numa_node), so that its pinned host buffers -- first touched here --
     sit next to the GPU's PCIe link.  Returns the node, or None (no sysfs, a visibility mask that
     renumbers the devices, or any error: the affinity is left alone)."""
-    if any(os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")):
+    if any(os.environ.get(v) for v in VISIBILITY_VARS):
         return None
     try:
-        base = "/sys/class/kfd/kfd/topology/nodes"
-        gpus = []
-        for d in sorted(os.listdir(base), key=int):
-            with open(f"{base}/{d}/properties") as f:
-                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
-            if int(props.get("simd_count", "0")) > 0:
-                gpus.append(props)
-        p = gpus[local_rank]
+        p = kfd_gpus()[local_rank]
         loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
         bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7}"
         with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
@@ -423,7 +451,7 @@ def launch_ranks(args, argv: list) -> int:
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                  HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
         envs.append(e)
-    visible = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+    visible = count_gpus()  # sysfs only: the launcher never initialises HIP (its workers do)
     if args.dry_run:
         keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                 "HSA_ENABLE_IPC_MODE_LEGACY")

@@ -31,7 +31,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "fastkmer.h")
 
 FK_OK = 0
 ERRORS = {-1: "FK_E_INVALID", -2: "FK_E_STATE", -3: "FK_E_DEVICE", -4: "FK_E_NOMEM", -5: "FK_E_IO",
-          -6: "FK_E_RANGE"}
+          -6: "FK_E_RANGE", -7: "FK_E_COMM"}
+ABI_VERSION = 3  # include/fastkmer.h FK_ABI_VERSION this binding mirrors (fk_config / fk_stats layouts)
 
 
 class FastKmerError(RuntimeError):
@@ -53,13 +54,12 @@ class fk_stats(ctypes.Structure):
                 ("ms_parse", "ms_signature", "ms_partition", "ms_count", "ms_total", "ms_encode_kernel",
                  "ms_signature_kernel")] + [("fused_map", ctypes.c_uint64), ("ms_h2d", ctypes.c_double),
                                        ("fused_fallback", ctypes.c_uint64),
-                                       ("ht_spilled", ctypes.c_uint64), ("ht_rounds", ctypes.c_uint64),
                                        ("xch_steps", ctypes.c_uint64), ("xch_bytes_sent", ctypes.c_uint64),
                                        ("xch_bytes_received", ctypes.c_uint64), ("ms_exchange", ctypes.c_double),
                                        ("ms_exchange_tail", ctypes.c_double),
-                                       ("pieces_counted", ctypes.c_uint64), ("ms_merge", ctypes.c_double),
+                                       ("pieces_counted", ctypes.c_uint64),
                                        ("heavy_keys", ctypes.c_uint64), ("block_buckets", ctypes.c_uint64), ("big_buckets", ctypes.c_uint64),
-                                       ("ht_big_groups", ctypes.c_uint64), ("split_buckets", ctypes.c_uint64),
+                                       ("split_buckets", ctypes.c_uint64),
                                        ("sub_buckets", ctypes.c_uint64)]
 
 COMM_ID_BYTES = 128
@@ -145,6 +145,8 @@ def lib():
         "fk_balance_bins_file": (ctypes.c_int, [P, ctypes.c_char_p, I32, I32, ctypes.c_double]),
         "fk_exchange_plan": (ctypes.c_int, [I32, I32, P, P, U64, P, P, P, P, P]),
         "fk_debug_map_cycles": (ctypes.c_int, [P, I32]),
+        "fk_debug_comm_hold": (ctypes.c_int, [P, I32]),
+        "fk_debug_comm_release": (ctypes.c_int, [P]),
         "fk_debug_wave_count": (ctypes.c_int, [I32, I32, I32, ctypes.c_uint32, ctypes.c_uint32, I32, P,
                                                ctypes.c_uint32, P, P, P]),
     }
@@ -152,6 +154,9 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.fk_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH} has ABI version {L.fk_abi_version()}, this binding mirrors {ABI_VERSION}: "
+                           "rebuild it (python -m fastkmer_amd.build)")
     _lib = L
     return L
 

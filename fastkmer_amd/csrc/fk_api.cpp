@@ -333,6 +333,8 @@ struct fk_ctx {
     std::vector<hipEvent_t> map_evs;  // ... and one "segment mapped" event (one rank's staged pieces)
     std::vector<uint64_t> seg_tiles;  // ... the tiles mapped once that segment's map is done
     PinBuf pin_up, pin_down;              // staging: chunk tables up, per-bin counts down
+    hipEvent_t pin_up_ev = nullptr;       // the last upload out of pin_up (on whichever stream queued it)
+    bool pin_up_busy = false;             // ... was queued and not yet waited for
     PinBuf pin_tier;                      // the bucket tiers' sizes, read while the wave tier runs
     PinBuf file_pin[2];                   // fk_ingest_file_range: the split read in pinned windows
     hipEvent_t tier_ev = nullptr;         // ... once this copy has landed
@@ -375,6 +377,7 @@ struct fk_ctx {
 
     fk::Comm *comm = nullptr;
     hipStream_t comm_stream = nullptr;
+    uint32_t *hold_flag = nullptr;               // fk_debug_comm_hold: host-mapped release flag
     // staging of received segments on its own stream (each waits for its step's transfer, so the map
     // stream never does) with its own scan workspace; the count waits for it
     hipStream_t xstage = nullptr;
@@ -410,6 +413,28 @@ struct fk_ctx {
 // ---------------------------------------------------------------------------
 
 FK_EXPORT int fk_abi_version(void) { return FK_ABI_VERSION; }
+
+// Host waits on work that may depend on the exchange (the comm stream, the staging stream that waits
+// for a step's transfer, events behind them): with a communicator they are bounded (Comm::wait: RCCL
+// polls, times out after FASTKMER_COMM_TIMEOUT_S and aborts the communicator) and fail with FK_E_COMM.
+static int comm_sync(fk_ctx *c, hipStream_t st) {
+    if (!c->comm) {
+        HIP_TRY(hipStreamSynchronize(st));
+        return FK_OK;
+    }
+    std::string err;
+    if (c->comm->wait(st, err)) return set_err(FK_E_COMM, "%s", err.c_str());
+    return FK_OK;
+}
+static int comm_event_sync(fk_ctx *c, hipEvent_t ev) {
+    if (!c->comm) {
+        HIP_TRY(hipEventSynchronize(ev));
+        return FK_OK;
+    }
+    std::string err;
+    if (c->comm->wait_event(ev, err)) return set_err(FK_E_COMM, "%s", err.c_str());
+    return FK_OK;
+}
 
 FK_EXPORT const char *fk_last_error(void) { return g_err.c_str(); }
 
@@ -590,6 +615,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
         }
     }
     e = hipEventCreateWithFlags(&c->tier_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->pin_up_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         fk_destroy(c);
         return set_err(FK_E_DEVICE, "hipEventCreate: %s", hipGetErrorString(e));
@@ -608,8 +634,11 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
 FK_EXPORT void fk_destroy(fk_ctx *c) {
     if (!c) return;
     DeviceGuard dg_(c->device);
+    if (c->hold_flag) __atomic_store_n(c->hold_flag, 1u, __ATOMIC_RELEASE);  // a test's held streams drain
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    // staged expansions (an ingest without fk_finish) read the buffers released below
+    if (c->xstage) (void)hipStreamSynchronize(c->xstage);
     DevBuf *bufs[] = {&c->fasta_own, &c->tile_last_nl, &c->tile_off,
                       &c->npos_dev, &c->codes, &c->valid, &c->records, &c->counters, &c->sig_status, &c->sig_kmers, &c->tcnt, &c->rec_hdr, &c->rec_pos, &c->rec_code, &c->tstat, &c->map_vslots,
                       &c->precs, &c->chunks, &c->bin_chunk_begin, &c->hpieces, &c->hpiece_first, &c->hpiece_tot, &c->chunk_nk, &c->grp_table,
@@ -632,6 +661,8 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     c->file_pin[0].release();
     c->file_pin[1].release();
     if (c->tier_ev) (void)hipEventDestroy(c->tier_ev);
+    if (c->pin_up_ev) (void)hipEventDestroy(c->pin_up_ev);
+    if (c->hold_flag) (void)hipHostFree(c->hold_flag);
     release(c->xsend);
     release(c->xrecv);
     for (auto &e : c->xev)
@@ -791,10 +822,10 @@ static int ingest_impl(fk_ctx *c, const uint8_t *fasta, size_t n, int last) {
         c->ingest_fresh = false;
         if (c->comm) {
             if (c->xch.open) return set_err(FK_E_STATE, "fk_ingest: the previous job's exchange is unfinished (fk_finish)");
-            HIP_TRY(hipStreamSynchronize(c->comm_stream));
+            FK_TRY(comm_sync(c, c->comm_stream));
             xch_reset(c);
         }
-        HIP_TRY(hipStreamSynchronize(c->xstage));
+        FK_TRY(comm_sync(c, c->xstage));
         HIP_TRY(hipStreamSynchronize(s));  // a previous job's work may still read the buffers
         pieces_reset(c);
         c->pm_active = premap_eligible(c);
@@ -1706,7 +1737,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             const uint32_t *l1 = lists + nbuckets;
             uint32_t *fbB = nullptr, *fbG = lists + nbuckets;  // the block / big-table kernels' lists
             uint32_t nfbB = 0, nfbG = ntier[1];
-            if (FK_SPLIT_HEAVY) {
+            if (FK_SPLIT_HEAVY && ntier[1]) {  // nothing to split: no split kernels, no read-back
                 const uint32_t nl = ntier[1];
                 const uint64_t maxsub = listed_keys / 64 + nl + 64;  // >= ceil(n / SPL_TGT) sub-buckets per bucket
                 FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
@@ -1956,13 +1987,18 @@ static int upload_chunks(fk_ctx *c, const std::vector<Chunk> &chunks, const std:
     const uint32_t nchunks = (uint32_t)chunks.size();
     FK_TRY(ensure(c->chunks, nchunks * sizeof(Chunk)));
     FK_TRY(ensure(c->bin_chunk_begin, ((uint64_t)c->nlb + 1) * 4));
-    // the previous upload through the staging buffer is complete: the count that used it synchronized
+    // the previous upload out of the staging buffer may still be queued (on the map stream, or on the
+    // staging stream behind a step's transfer): wait for it before the host overwrites the buffer
+    if (c->pin_up_busy) FK_TRY(comm_event_sync(c, c->pin_up_ev));
+    c->pin_up_busy = false;
     const size_t cb = (size_t)nchunks * sizeof(Chunk), bb = ((size_t)c->nlb + 1) * 4;
     if (c->pin_up.ensure(cb + bb)) return set_err(FK_E_NOMEM, "hipHostMalloc(%zu) failed", cb + bb);
     memcpy(c->pin_up.p, chunks.data(), cb);
     memcpy(c->pin_up.as<uint8_t>() + cb, bcb.data(), bb);
     if (nchunks) HIP_TRY(hipMemcpyAsync(c->chunks.p, c->pin_up.p, cb, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->bin_chunk_begin.p, c->pin_up.as<uint8_t>() + cb, bb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(c->pin_up_ev, s));
+    c->pin_up_busy = true;
     c->h_bcb = bcb;
     return FK_OK;
 }
@@ -2238,7 +2274,6 @@ static int staged_count(fk_ctx *c) {
     }
     c->stats.ms_partition = mp;
     c->stats.ms_count = mx + ev_ms(c->ev[6], c->ev[7]);
-    c->stats.ms_merge = 0.0;
     c->stats.pieces_counted = c->st_np;
     c->stats.records_received = c->nrec;
     c->stats.distinct = c->distinct;
@@ -2423,7 +2458,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
     if (piece_rec) {
         // send ring: earlier pieces are read by the comm stream; wrap around once it has drained
         if ((c->xch.send_used + piece_rec) * rb > c->xsend.bytes) {
-            HIP_TRY(hipStreamSynchronize(cs));
+            FK_TRY(comm_sync(c, cs));
             c->xch.send_used = 0;
             FK_TRY(ensure(c->xsend, piece_rec * rb * 2));
         }
@@ -2441,7 +2476,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
     }
     std::string err;
     if (c->comm->alltoall_u64(out.data(), in.data(), msg, cs, err))
-        return set_err(FK_E_DEVICE, "exchange step %llu, counts: %s", (unsigned long long)c->xch.pieces, err.c_str());
+        return set_err(FK_E_COMM, "exchange step %llu, counts: %s", (unsigned long long)c->xch.pieces, err.c_str());
     std::vector<uint64_t> soff(G), sbytes(G), roff(G), rbytes(G);
     bool all_final = false;
     FK_TRY(plan_step(G, L, out.data(), in.data(), rb, soff.data(), sbytes.data(), roff.data(), rbytes.data(), &all_final));
@@ -2455,8 +2490,8 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
             const double covered = (double)c->xch.tiles_sent * (double)fm_tile_bytes(FUSED_NT);
             want = std::max<uint64_t>(want, (uint64_t)((double)want * (double)c->xch.expect_bytes / covered * 1.1));
         }
-        HIP_TRY(hipStreamSynchronize(cs));
-        HIP_TRY(hipStreamSynchronize(c->xstage));  // staged expansions may still read the old buffer
+        FK_TRY(comm_sync(c, cs));
+        FK_TRY(comm_sync(c, c->xstage));  // staged expansions may still read the old buffer
         FK_TRY(grow_keep(c->xrecv, want * rb, c->xch.recv_used * rb, s));
     }
     const size_t step = (size_t)c->xch.pieces;
@@ -2466,7 +2501,7 @@ static int xch_step(fk_ctx *c, const RecSrc *src, uint64_t flags) {
     HIP_TRY(hipEventRecord(e0, cs));
     if (c->comm->alltoallv(c->xsend.as<uint8_t>() + c->xch.send_used * rb, soff.data(), sbytes.data(),
                            c->xrecv.as<uint8_t>() + c->xch.recv_used * rb, roff.data(), rbytes.data(), cs, err))
-        return set_err(FK_E_DEVICE, "exchange step %llu, records: %s", (unsigned long long)step, err.c_str());
+        return set_err(FK_E_COMM, "exchange step %llu, records: %s", (unsigned long long)step, err.c_str());
     HIP_TRY(hipEventRecord(e1, cs));
     for (uint32_t r = 0; r < G; ++r) {
         const uint64_t *m = in.data() + (size_t)r * msg;
@@ -2531,8 +2566,8 @@ static int xch_stage_segments(fk_ctx *c, size_t s1, double frac) {
     if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
     StageStream ss_(c);
     hipStream_t s = c->stream;  // the staging stream
-    // the chunk table goes up through the pinned staging buffer: the last upload from it is done
-    HIP_TRY(hipStreamSynchronize(s));
+    // its earlier work (behind earlier steps' transfers) is done: bounded with a communicator
+    FK_TRY(comm_sync(c, s));
     const uint64_t step = c->xch.segs[s1 - 1].step;
     HIP_TRY(hipStreamWaitEvent(s, c->xev[2 * step + 1], 0));
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ranges;
@@ -2624,6 +2659,9 @@ static int finish_exchange(fk_ctx *c) {
     int rc = xch_step(c, &src, flags);
     const size_t last_step = (size_t)c->xch.pieces - 1;
     while (!rc && !c->xch.all_final) rc = xch_step(c, nullptr, XF_FINAL);
+    // every transfer of the job has been posted; the host waits for them here, bounded, so that none
+    // of the count's host waits below can block on a peer that died (FK_E_COMM instead)
+    if (!rc) rc = comm_sync(c, cs);
     if (rc) return comm_fail(c, rc);
     HIP_TRY(hipEventRecord(c->ev[4], cs));  // every rank's records have landed
     HIP_TRY(hipStreamWaitEvent(s, c->ev[4], 0));
@@ -2767,7 +2805,7 @@ FK_EXPORT int fk_comm_allreduce_u64(fk_ctx *c, uint64_t *v, size_t n) {
     if (!c->comm) return set_err(FK_E_STATE, "fk_comm_allreduce_u64 needs a communicator (fk_comm_init*)");
     DeviceGuard dg_(c->device);
     std::string err;
-    if (c->comm->allreduce_sum_u64(v, n, c->comm_stream, err)) return comm_fail(c, set_err(FK_E_DEVICE, "%s", err.c_str()));
+    if (c->comm->allreduce_sum_u64(v, n, c->comm_stream, err)) return comm_fail(c, set_err(FK_E_COMM, "%s", err.c_str()));
     return FK_OK;
 }
 
@@ -2805,7 +2843,7 @@ static int balance_from_sample(fk_ctx *c, const uint8_t *sample, size_t n) {
     if (c->comm) {
         std::string err;
         if (c->comm->allreduce_sum_u64(sizes.data(), sizes.size(), c->comm_stream, err))
-            return set_err(FK_E_DEVICE, "bin size all-reduce: %s", err.c_str());
+            return set_err(FK_E_COMM, "bin size all-reduce: %s", err.c_str());
     }
     std::vector<int32_t> owner((size_t)c->Bc);
     FK_TRY(fk_lpt_owners(sizes.data(), c->Bc, (int32_t)c->G, owner.data()));
@@ -2964,6 +3002,36 @@ FK_EXPORT int fk_get_bin(fk_ctx *c, int32_t bin, uint64_t *keys, uint32_t *count
     if (keys)
         HIP_TRY(hipMemcpy(keys, c->dense_keys.as<uint64_t>() + b0 * c->KW, cnt * 8 * c->KW, hipMemcpyDeviceToHost));
     if (counts) HIP_TRY(hipMemcpy(counts, c->dense_counts.as<uint32_t>() + b0, cnt * 4, hipMemcpyDeviceToHost));
+    return FK_OK;
+}
+
+// Test hooks of the failure semantics (fastkmer.h): hold every stream the context's collectives run
+// on with a kernel spinning on a host-mapped flag, so the next collective waits on a stream that does
+// not drain; release it from any thread.
+FK_EXPORT int fk_debug_comm_hold(fk_ctx *c, int32_t max_seconds) {
+    if (!c || max_seconds < 1) return set_err(FK_E_INVALID, "bad argument");
+    if (!c->comm) return set_err(FK_E_STATE, "fk_debug_comm_hold needs a communicator (fk_comm_init*)");
+    DeviceGuard dg_(c->device);
+    if (!c->hold_flag) {
+        void *p = nullptr;
+        HIP_TRY(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        c->hold_flag = static_cast<uint32_t *>(p);
+    }
+    __atomic_store_n(c->hold_flag, 0u, __ATOMIC_RELEASE);
+    void *dflag = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dflag, c->hold_flag, 0));
+    int khz = 0;
+    HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    const uint64_t ticks = (uint64_t)max_seconds * (uint64_t)std::max(khz, 1) * 1000ull;
+    const hipStream_t cs2 = c->comm->counts_stream();
+    for (hipStream_t st : {c->comm_stream, cs2})
+        if (st) HIP_TRY(launch_hold_stream(static_cast<const uint32_t *>(dflag), ticks, st));
+    return FK_OK;
+}
+
+FK_EXPORT int fk_debug_comm_release(fk_ctx *c) {
+    if (!c) return set_err(FK_E_INVALID, "null ctx");
+    if (c->hold_flag) __atomic_store_n(c->hold_flag, 1u, __ATOMIC_RELEASE);
     return FK_OK;
 }
 

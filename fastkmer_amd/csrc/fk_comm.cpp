@@ -7,6 +7,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+#include <unistd.h>
+
+#include <chrono>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -49,6 +53,7 @@ struct RcclApi {
     ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
     const char *(*GetErrorString)(ncclResult_t) = nullptr;
+    ncclResult_t (*GetAsyncError)(ncclComm_t, ncclResult_t *) = nullptr;  // optional
 };
 
 std::mutex g_rccl_mu;
@@ -87,6 +92,7 @@ const RcclApi *rccl(std::string &err) {
             SYM(Recv, "ncclRecv");
             SYM(AllReduce, "ncclAllReduce");
             SYM(GetErrorString, "ncclGetErrorString");
+            SYM(GetAsyncError, "ncclCommGetAsyncError");
 #undef SYM
             if (a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
                 a.AllReduce && a.GetErrorString) {
@@ -111,27 +117,34 @@ const RcclApi *rccl(std::string &err) {
 // (ncclCommSplit) with a stream and staging buffer of their own -- so a step's count exchange does
 // not queue behind the previous step's records still moving on the comm stream (RCCL orders the
 // operations of one communicator across streams).  Every rank issues both kinds in the same order.
-// Without ncclCommSplit both run on the one communicator and the caller's stream.
+// Without ncclCommSplit, or with FASTKMER_COMM_SPLIT=0, both run on the one communicator and the
+// caller's stream.
+//
+// Failure semantics: a Spark job fails when one of its tasks fails (SBKC:1031-1043); here a rank
+// that dies mid-exchange must not leave its peers blocked.  Every host wait on RCCL work goes
+// through wait(): it polls the stream and ncclCommGetAsyncError, and after timeout_s_ (or on an
+// asynchronous error) aborts both communicators -- RCCL kernels waiting for the dead peer then
+// exit -- and fails; later calls fail at once.
 class RcclComm : public Comm {
    public:
-    RcclComm(const RcclApi *api, ncclComm_t comm, int n, int rank) : api_(api), comm_(comm) {
+    RcclComm(const RcclApi *api, ncclComm_t comm, int n, int rank, double timeout_s)
+        : api_(api), comm_(comm), timeout_s_(timeout_s) {
         n_ = n;
         rank_ = rank;
     }
     ~RcclComm() override {
+        if (cstream_) (void)hipStreamSynchronize(cstream_);
         if (stage_) (void)hipFree(stage_);
-        if (cstream_) {
-            (void)hipStreamSynchronize(cstream_);
-            (void)hipStreamDestroy(cstream_);
-        }
+        if (cstream_) (void)hipStreamDestroy(cstream_);
         if (ccomm_) (void)api_->CommDestroy(ccomm_);
         if (comm_) (void)api_->CommDestroy(comm_);
     }
     const char *kind() const override { return "rccl"; }
+    hipStream_t counts_stream() const override { return cstream_; }
 
     // collective over the ranks (every rank calls it once, right after joining)
-    int init_counts(std::string &err) {
-        if (!api_->CommSplit) return 0;
+    int init_counts(bool split, std::string &err) {
+        if (!api_->CommSplit || !split) return 0;
         ncclComm_t c2 = nullptr;
         if (nccl(api_->CommSplit(comm_, 0, rank_, &c2, nullptr), err)) return -1;
         ccomm_ = c2;
@@ -140,10 +153,11 @@ class RcclComm : public Comm {
     }
 
     int alltoall_u64(const uint64_t *in, uint64_t *out, size_t n, hipStream_t s, std::string &err) override {
+        if (dead(err)) return -1;
         ncclComm_t cm = ccomm_ ? ccomm_ : comm_;
         if (cstream_) s = cstream_;
         const size_t bytes = (size_t)n_ * n * 8;
-        if (stage(2 * bytes, err)) return -1;
+        if (stage(2 * bytes, s, err)) return -1;
         uint64_t *din = static_cast<uint64_t *>(stage_), *dout = din + (size_t)n_ * n;
         COMM_HIP(hipMemcpyAsync(din, in, bytes, hipMemcpyHostToDevice, s));
         if (nccl(api_->GroupStart(), err)) return -1;
@@ -153,24 +167,24 @@ class RcclComm : public Comm {
         }
         if (nccl(api_->GroupEnd(), err)) return -1;
         COMM_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s));
-        COMM_HIP(hipStreamSynchronize(s));
-        return 0;
+        return wait(s, err);
     }
 
     int allreduce_sum_u64(uint64_t *v, size_t n, hipStream_t s, std::string &err) override {
+        if (dead(err)) return -1;
         if (!n) return 0;
         ncclComm_t cm = ccomm_ ? ccomm_ : comm_;
         if (cstream_) s = cstream_;
-        if (stage(n * 8, err)) return -1;
+        if (stage(n * 8, s, err)) return -1;
         COMM_HIP(hipMemcpyAsync(stage_, v, n * 8, hipMemcpyHostToDevice, s));
         if (nccl(api_->AllReduce(stage_, stage_, n, ncclUint64, ncclSum, cm, s), err)) return -1;
         COMM_HIP(hipMemcpyAsync(v, stage_, n * 8, hipMemcpyDeviceToHost, s));
-        COMM_HIP(hipStreamSynchronize(s));
-        return 0;
+        return wait(s, err);
     }
 
     int alltoallv(const uint8_t *send, const uint64_t *soff, const uint64_t *sbytes, uint8_t *recv,
                   const uint64_t *roff, const uint64_t *rbytes, hipStream_t s, std::string &err) override {
+        if (dead(err)) return -1;
         if (nccl(api_->GroupStart(), err)) return -1;
         for (int p = 0; p < n_; ++p) {
             // a pair with nothing to move posts nothing on either side (both know the size)
@@ -182,7 +196,17 @@ class RcclComm : public Comm {
         return nccl(api_->GroupEnd(), err);
     }
 
+    // Bounded host waits (see the class comment).  The first ~2 ms spin on the query (the per-step
+    // waits are short), then the poll sleeps 50 us between queries.
+    int wait(hipStream_t s, std::string &err) override {
+        return poll([s] { return hipStreamQuery(s); }, "hipStreamQuery", err);
+    }
+    int wait_event(hipEvent_t ev, std::string &err) override {
+        return poll([ev] { return hipEventQuery(ev); }, "hipEventQuery", err);
+    }
+
     void abort() override {
+        aborted_ = true;
         if (ccomm_ && api_->CommAbort) {
             (void)api_->CommAbort(ccomm_);
             ccomm_ = nullptr;
@@ -206,7 +230,63 @@ class RcclComm : public Comm {
         (void)err;
         return -1;
     }
-    int stage(size_t bytes, std::string &err) {
+    bool dead(std::string &err) const {
+        if (!aborted_) return false;
+        err = "RCCL: the communicator was aborted by an earlier failure of this job";
+        return true;
+    }
+    // an asynchronous error on either communicator (a peer's failure seen by RCCL's proxy)
+    bool async_error(std::string &err) {
+        if (!api_->GetAsyncError) return false;
+        for (ncclComm_t cm : {comm_, ccomm_}) {
+            if (!cm) continue;
+            ncclResult_t ar = ncclSuccess;
+            if (api_->GetAsyncError(cm, &ar) != ncclSuccess) continue;
+            if (ar != ncclSuccess && ar != ncclInProgress) {
+                err = std::string("RCCL asynchronous error: ") + api_->GetErrorString(ar);
+                return true;
+            }
+        }
+        return false;
+    }
+    template <typename Q>
+    int poll(Q query, const char *what, std::string &err) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        for (uint64_t it = 0;; ++it) {
+            const hipError_t q = query();
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady) {
+                err = hip_msg(what, q);
+                abort();
+                return -1;
+            }
+            if ((it & 63) != 63) {
+                sched_yield();
+                continue;
+            }
+            if (async_error(err)) {
+                abort();
+                return -1;
+            }
+            const double el = std::chrono::duration<double>(clk::now() - t0).count();
+            if (timeout_s_ > 0 && el > timeout_s_) {
+                char msg[192];
+                snprintf(msg, sizeof msg,
+                         "RCCL: timed out after %.0f s waiting for rank %d's collective work "
+                         "(FASTKMER_COMM_TIMEOUT_S); communicator aborted",
+                         timeout_s_, rank_);
+                err = msg;
+                abort();
+                return -1;
+            }
+            if (el > 0.002) usleep(50);
+        }
+    }
+    // the staging buffer of the small collectives; the stream that last used it has drained (every
+    // collective ends in a wait on it), so it can be replaced
+    int stage(size_t bytes, hipStream_t s, std::string &err) {
+        (void)s;
         if (stage_bytes_ >= bytes) return 0;
         if (stage_) (void)hipFree(stage_);
         stage_ = nullptr;
@@ -221,6 +301,8 @@ class RcclComm : public Comm {
     hipStream_t cstream_ = nullptr; // ... and its stream
     void *stage_ = nullptr;
     size_t stage_bytes_ = 0;
+    double timeout_s_;
+    bool aborted_ = false;
 };
 
 // ---------------------------------------------------------------------------
@@ -413,8 +495,12 @@ Comm *comm_create_rccl(const uint8_t id[COMM_ID_BYTES], int n, int rank, int dev
         return nullptr;
     }
     (void)device;
-    auto *rc = new RcclComm(a, comm, n, rank);
-    if (rc->init_counts(err)) {
+    double timeout = 120.0;
+    if (const char *e = getenv("FASTKMER_COMM_TIMEOUT_S"); e && e[0]) timeout = atof(e);
+    const char *sp = getenv("FASTKMER_COMM_SPLIT");
+    const bool split = !(sp && sp[0] == '0');
+    auto *rc = new RcclComm(a, comm, n, rank, timeout);
+    if (rc->init_counts(split, err)) {
         delete rc;
         return nullptr;
     }

@@ -44,6 +44,28 @@ class Comm {
     // Marks the group failed so that peers blocked in a collective return an
     // error instead of waiting (in-process groups; RCCL aborts the communicator).
     virtual void abort() {}
+    // Host wait for everything queued on `s` (which may hold this transport's
+    // work).  RCCL: bounded -- polls the stream and the communicators'
+    // asynchronous error; after the timeout (FASTKMER_COMM_TIMEOUT_S) or on an
+    // RCCL error it aborts the communicators and returns -1 with `err` set.
+    virtual int wait(hipStream_t s, std::string &err) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e == hipSuccess) return 0;
+        (void)hipGetLastError();
+        err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
+        return -1;
+    }
+    // The same for one event.
+    virtual int wait_event(hipEvent_t ev, std::string &err) {
+        const hipError_t e = hipEventSynchronize(ev);
+        if (e == hipSuccess) return 0;
+        (void)hipGetLastError();
+        err = std::string("hipEventSynchronize: ") + hipGetErrorString(e);
+        return -1;
+    }
+    // The stream the small host-array collectives run on when it is not the
+    // caller's (RCCL with a split counts communicator), else null.
+    virtual hipStream_t counts_stream() const { return nullptr; }
 
    protected:
     int n_ = 1, rank_ = 0;
@@ -52,6 +74,8 @@ class Comm {
 // A fresh RCCL unique id (ncclGetUniqueId): created on one rank, handed to all.
 int comm_unique_id(uint8_t id[COMM_ID_BYTES], std::string &err);
 // Joins the RCCL communicator of `n` ranks as `rank` on HIP device `device`.
+// Environment: FASTKMER_COMM_TIMEOUT_S (bounded waits, default 120 s; 0 = unbounded),
+// FASTKMER_COMM_SPLIT=0 (the counts on the records' communicator and stream).
 Comm *comm_create_rccl(const uint8_t id[COMM_ID_BYTES], int n, int rank, int device, std::string &err);
 // n ranks in this process (devices[r] = rank r's HIP device): out[r] = rank r's Comm.
 int comm_create_local(int n, const int *devices, Comm **out, std::string &err);

@@ -286,6 +286,10 @@ hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_
 hipError_t launch_bin_offsets(const uint64_t *flag_scan, const uint64_t *dense_off, uint32_t nlbins, int F,
                               uint64_t nbuckets, uint64_t *bin_off, hipStream_t s);
 
+// ---- test hook: a one-thread kernel holding stream s until *flag != 0 (host-mapped) or max_ticks
+// of the wall clock have passed
+hipError_t launch_hold_stream(const uint32_t *flag, uint64_t max_ticks, hipStream_t s);
+
 // ---- synthetic input
 hipError_t launch_synth(uint8_t *out, uint64_t nbytes, SynthParams p, hipStream_t s);
 

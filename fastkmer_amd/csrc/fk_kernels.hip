@@ -342,4 +342,21 @@ hipError_t scan_excl_max_i64(const int64_t *in, int64_t *out, uint64_t n, ScanWo
 #include "fk_synth.inc"
 #include "fk_format.inc"
 #include "fk_bin_signatures.inc"
+
+// Test hook of the failure semantics (fk_debug_comm_hold): one thread spins on a host-mapped flag
+// with s_sleep between its system-scope loads, and leaves by itself after max_ticks of the 100 MHz
+// wall clock, so the stream it holds always drains.
+__global__ void __launch_bounds__(64) k_hold_stream(const uint32_t *flag, uint64_t max_ticks) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+        if (wall_clock64() - t0 > max_ticks) break;
+        __builtin_amdgcn_s_sleep(127);
+    }
+}
+
+hipError_t launch_hold_stream(const uint32_t *flag, uint64_t max_ticks, hipStream_t s) {
+    hipLaunchKernelGGL(k_hold_stream, dim3(1), dim3(64), 0, s, flag, max_ticks);
+    return hipGetLastError();
+}
 }  // namespace fk

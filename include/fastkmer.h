@@ -25,7 +25,12 @@
 extern "C" {
 #endif
 
-#define FK_ABI_VERSION 2
+/* ABI version policy: bumped whenever an exported signature, a struct layout
+ * (fk_config, fk_stats) or an error code's meaning changes; callers compare
+ * fk_abi_version() with the FK_ABI_VERSION they were built against.
+ *   3: fk_stats lost four always-zero fields (ht_spilled, ht_rounds, ms_merge,
+ *      ht_big_groups); FK_E_COMM; fk_debug_comm_hold / fk_debug_comm_release. */
+#define FK_ABI_VERSION 3
 
 #define FK_OK 0
 #define FK_E_INVALID (-1) /* bad argument or configuration (reference: require / AIOOBE) */
@@ -34,6 +39,9 @@ extern "C" {
 #define FK_E_NOMEM (-4)   /* device or host allocation failed */
 #define FK_E_IO (-5)      /* file system error while writing bins */
 #define FK_E_RANGE (-6)   /* caller buffer too small / bin out of range */
+#define FK_E_COMM (-7)    /* a collective of the job failed or timed out (FASTKMER_COMM_TIMEOUT_S); the
+                             communicator is aborted, later collective calls fail fast (reference: a failed
+                             task fails the Spark job, SBKC:1031-1043) */
 
 /* Mirrors skc.test.testutil.TestConfiguration (test/package.scala:16-42). */
 typedef struct fk_config {
@@ -74,8 +82,6 @@ typedef struct fk_stats {
     double ms_h2d;             /* last fk_ingest: host-to-device copy, first segment issued to last landed */
     uint64_t fused_fallback;   /* why the fused kernel handed the input back: 1 long line, 2 text before the
                                   first header, 4 halo too short, 8 too many records in a tile (0: none) */
-    uint64_t ht_spilled;       /* unused (0): the useHT group tables are gone (useHT counts buckets) */
-    uint64_t ht_rounds;        /* unused (0) */
     /* multi-rank exchange inside the context (fk_comm_init*), last fk_finish */
     uint64_t xch_steps;        /* exchange steps (pieces sent during fk_ingest, the last piece, closing steps) */
     uint64_t xch_bytes_sent;   /* record bytes sent to other ranks */
@@ -84,13 +90,11 @@ typedef struct fk_stats {
     double ms_exchange_tail;   /* fk_finish: the last piece posted -> every rank's records received */
     /* pieces counted while later ones were still being copied in / received (sorted count) */
     uint64_t pieces_counted;   /* staged pieces of the last fk_finish (0: one count of the whole input) */
-    double ms_merge;           /* unused (0): staged pieces are counted once, never merged */
     uint64_t heavy_keys;       /* sorted count: k-mers in the buckets above the wave tier (split or block / big) */
     uint64_t block_buckets;    /* block tier: buckets above the wave tier of at most 1024 keys (k <= 32: the mid wave
                                   tier) / 2048 keys (k > 32: mid wave tier, LDS sort) */
     uint64_t big_buckets;      /* above the block tier (k <= 32: split into sub-buckets, fallbacks to the block /
                                   big-table kernels; k > 32: the streaming path) */
-    uint64_t ht_big_groups;    /* unused (0) */
     uint64_t split_buckets;    /* k <= 32: buckets above the wave tier split into wave-sized sub-buckets */
     uint64_t sub_buckets;      /* ... into this many sub-buckets (the wave tier counted them) */
 } fk_stats;
@@ -224,7 +228,17 @@ int fk_bin_owners(const fk_ctx *ctx, int32_t *owner);
  * fk_ingest, which may send pieces) are collective: every rank of the job
  * calls them, each from its own host thread or process.  Ranks may hold
  * different amounts of input: a rank that has sent its last piece keeps
- * answering the others' steps inside fk_finish. */
+ * answering the others' steps inside fk_finish.
+ * Failure semantics (the reference fails the whole Spark job when one task
+ * fails: require at package.scala:182,185, exceptions out of SBKC:1031-1043):
+ * every host wait on RCCL work is bounded -- it polls the stream and
+ * ncclCommGetAsyncError, and after FASTKMER_COMM_TIMEOUT_S seconds (default
+ * 120) or an asynchronous RCCL error it aborts the communicator
+ * (ncclCommAbort) and the call returns FK_E_COMM; any failing collective call
+ * aborts it too, so the peers' waits end instead of blocking.
+ * FASTKMER_COMM_SPLIT=0 keeps the per-step count exchange on the records'
+ * communicator and stream (default: a communicator split off it, with its own
+ * stream). */
 #define FK_COMM_ID_BYTES 128
 /* A fresh RCCL unique id (ncclGetUniqueId): made on one rank, handed to all. */
 int fk_comm_unique_id(uint8_t id[FK_COMM_ID_BYTES]);
@@ -287,6 +301,16 @@ int fk_get_stats(fk_ctx *ctx, fk_stats *out);
 int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t c0, uint32_t c1, int32_t slots,
                         const uint64_t *keys, uint32_t n, uint64_t *out_keys, uint32_t *out_counts,
                         uint32_t *n_out);
+
+/* ---- test hooks of the failure semantics (no reference counterpart) ----
+ * fk_debug_comm_hold queues, on every stream the context's collectives run on,
+ * a one-thread kernel that spins on a host-mapped flag (it ends by itself after
+ * max_seconds), so that the next collective call waits on a stream that does
+ * not drain -- what a rank blocked by a dead peer sees.  fk_debug_comm_release
+ * sets the flag (callable from another thread while a collective is waiting);
+ * fk_destroy releases it too. */
+int fk_debug_comm_hold(fk_ctx *ctx, int32_t max_seconds);
+int fk_debug_comm_release(fk_ctx *ctx);
 
 /* Measurement hook: per-phase wave cycles of the fused map kernel summed over
  * its launches since the last reset (out[0..16)); only a library built with

@@ -44,6 +44,10 @@ def lib():
         L.fko_count.restype = ctypes.c_void_p
         L.fko_count_mt.argtypes = L.fko_count.argtypes + [ctypes.c_int32]
         L.fko_count_mt.restype = ctypes.c_void_p
+        L.fko_count_mt_filtered.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32]
+        L.fko_count_mt_filtered.restype = ctypes.c_void_p
         for name in ("fko_total_kmers", "fko_superkmers", "fko_reads", "fko_distinct"):
             getattr(L, name).argtypes = [ctypes.c_void_p]
             getattr(L, name).restype = ctypes.c_int64
@@ -99,13 +103,28 @@ def kmer_to_string(hi: int, lo: int, k: int) -> str:
 class OracleResult:
     """Per-bin sorted (canonical k-mer, count) lists computed on the CPU."""
 
-    def __init__(self, fasta: bytes, k: int, m: int, B: int, sequence_type: int = 0, threads: int = 1):
+    def __init__(self, fasta: bytes, k: int, m: int, B: int, sequence_type: int = 0, threads: int = 1,
+                 bin_mod: int = 0, bin_rem: int = 0, ptr: int = 0, nbytes: int = 0):
+        """fasta: the input bytes, or (fasta=None) `nbytes` bytes at address `ptr` (e.g. a pinned
+        multi-GB buffer, read in place).  bin_mod > 0 keeps only the bins b % bin_mod == bin_rem
+        (the others are walked and counted in total_kmers, not stored): a memory bound for checks
+        at the full per-GPU loads."""
         L = lib()
         self.k, self.m = k, m
-        self._buf = bytes(fasta)
-        if threads > 1:
+        self.bin_mod, self.bin_rem = bin_mod, bin_rem
+        if fasta is None:
+            self._buf = None
+            h = L.fko_count_mt_filtered(ctypes.c_void_p(ptr), nbytes, k, m, B, sequence_type, max(1, threads),
+                                        bin_mod, bin_rem)
+        elif bin_mod:
+            self._buf = bytes(fasta)
+            h = L.fko_count_mt_filtered(ctypes.cast(ctypes.c_char_p(self._buf), ctypes.c_void_p), len(self._buf),
+                                        k, m, B, sequence_type, max(1, threads), bin_mod, bin_rem)
+        elif threads > 1:
+            self._buf = bytes(fasta)
             h = L.fko_count_mt(self._buf, len(self._buf), k, m, B, sequence_type, threads)
         else:
+            self._buf = bytes(fasta)
             h = L.fko_count(self._buf, len(self._buf), k, m, B, sequence_type)
         if not h:
             raise ValueError(f"invalid oracle parameters k={k} m={m} B={B}")

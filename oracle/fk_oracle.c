@@ -167,6 +167,8 @@ static void bin_push(fko_bin *b, u128 key) {
 typedef struct {
     int32_t k, m, B;
     const int32_t *norm; /* fillNorm table, or NULL -> computed per call */
+    int32_t bin_mod, bin_rem; /* keep only bins b with b % bin_mod == bin_rem (bin_mod 0: every bin);
+                                 a checker's memory bound at large sizes, not part of the reference */
 } fko_params;
 
 static inline int32_t norm_of(const fko_params *p, int32_t v) {
@@ -242,6 +244,11 @@ static void emit_superkmer(fko_result *r, const fko_params *p, const uint8_t *cu
         r->trace_start[r->superkmers] = start;
         r->trace_len[r->superkmers] = len;
         r->trace_bin[r->superkmers] = bin;
+    }
+    if (p->bin_mod > 0 && bin % p->bin_mod != p->bin_rem) { /* filtered out: counted, not kept */
+        r->total_kmers += len - p->k + 1;
+        r->superkmers++;
+        return;
     }
     for (int64_t i = start; i + p->k <= start + len; ++i) {
         bin_push(b, canonical_at(cur, i, p->k));
@@ -384,6 +391,8 @@ FKO_API fko_result *fko_count(const uint8_t *fasta, size_t n, int32_t k, int32_t
     p.k = k;
     p.m = m;
     p.B = fko_clamp_bins(m, B);
+    p.bin_mod = 0;
+    p.bin_rem = 0;
     int32_t *norm = NULL;
     if (m <= 12) { /* fillNorm table (package.scala:77-100), per task (SBKC:47) */
         int64_t sz = (int64_t)1 << (2 * m);
@@ -454,15 +463,21 @@ static void *mt_reduce(void *arg) {
     return NULL;
 }
 
-FKO_API fko_result *fko_count_mt(const uint8_t *fasta, size_t n, int32_t k, int32_t m, int32_t B,
-                                 int32_t sequence_type, int32_t nthreads) {
+/* fko_count_mt keeping only the bins b % bin_mod == bin_rem (bin_mod 0: all): the other bins' k-mers
+ * are walked and counted in total_kmers / superkmers but never canonicalised or stored, so a checker
+ * holds 1 / bin_mod of a multi-GB job's keys (tests/test_gpu_configs.py, the configs[2] per-GPU load). */
+FKO_API fko_result *fko_count_mt_filtered(const uint8_t *fasta, size_t n, int32_t k, int32_t m, int32_t B,
+                                          int32_t sequence_type, int32_t nthreads, int32_t bin_mod, int32_t bin_rem) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     if (k < 1 || k > 64 || m < 1 || m > 15 || m > k || B < 1) return NULL;
+    if (bin_mod < 0 || (bin_mod > 0 && (bin_rem < 0 || bin_rem >= bin_mod))) return NULL;
     fko_params p;
     p.k = k;
     p.m = m;
     p.B = fko_clamp_bins(m, B);
+    p.bin_mod = bin_mod;
+    p.bin_rem = bin_rem;
     int32_t *norm = NULL;
     if (m <= 12) {
         int64_t sz = (int64_t)1 << (2 * m);
@@ -514,6 +529,11 @@ FKO_API fko_result *fko_count_mt(const uint8_t *fasta, size_t n, int32_t k, int3
     free(norm);
     (void)sequence_type;
     return r;
+}
+
+FKO_API fko_result *fko_count_mt(const uint8_t *fasta, size_t n, int32_t k, int32_t m, int32_t B,
+                                 int32_t sequence_type, int32_t nthreads) {
+    return fko_count_mt_filtered(fasta, n, k, m, B, sequence_type, nthreads, 0, 0);
 }
 
 FKO_API int32_t fko_nbins(const fko_result *r) { return r->nbins; }
@@ -598,6 +618,7 @@ FKO_API int64_t fko_trace_read(const uint8_t *read, int64_t n, int32_t k, int32_
     p.m = m;
     p.B = fko_clamp_bins(m, B);
     p.norm = NULL;
+    p.bin_mod = p.bin_rem = 0;
     fko_result r;
     memset(&r, 0, sizeof(r));
     r.k = k;
@@ -685,6 +706,7 @@ FKO_API int fko_bin_signatures(const uint8_t *fasta, size_t n, int32_t k, int32_
     p.m = m;
     p.B = 1;
     p.norm = NULL;
+    p.bin_mod = p.bin_rem = 0;
     memset(counts, 0, (((size_t)1 << (2 * m)) + 1) * sizeof(int64_t));
     sig_ctx c = {counts, &p};
     for_each_read(fasta, n, sig_read, &c);

@@ -10,5 +10,5 @@ for i in range(3):
 st = kc.stats()
 print(f"count {st['ms_count']:.2f} ms  partition {st['ms_partition']:.2f}  buckets {st['buckets']} F {st['fine_bits']} "
       f"oversize {st['oversize_buckets']} kmers {st['kmers']} distinct {st['distinct']}"
-      f"{' ht_spilled %d ht_rounds %d' % (st['ht_spilled'], st['ht_rounds']) if os.environ.get('FK_HT') == '1' else ''}",
+      f"{' ht_spilled %d ht_rounds %d' % (st.get('ht_spilled', 0), st.get('ht_rounds', 0)) if os.environ.get('FK_HT') == '1' else ''}",
       flush=True)

@@ -17,5 +17,5 @@ for it in range(3):
     kc.finish()
     st = kc.stats()
     print(f"LDS_HT={os.environ.get('FASTKMER_LDS_HT', '1')} k={k}: count {st['ms_count']:.2f} ms partition "
-          f"{st['ms_partition']:.2f} rounds {st['ht_rounds']} spilled {st['ht_spilled']} distinct {st['distinct']} "
+          f"{st['ms_partition']:.2f} rounds {st.get('ht_rounds', 0)} spilled {st.get('ht_spilled', 0)} distinct {st['distinct']} "
           f"kmers {st['kmers']} big {st.get('ht_big_groups', 0)}", flush=True)

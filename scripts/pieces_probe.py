@@ -32,7 +32,7 @@ for arg in sys.argv[1:]:
         kc.finish()
         t2 = time.perf_counter()
         st = kc.stats()
-        rows.append(((t1 - t0) * 1e3, (t2 - t1) * 1e3, st["ms_h2d"], st["pieces_counted"], st["ms_merge"],
+        rows.append(((t1 - t0) * 1e3, (t2 - t1) * 1e3, st["ms_h2d"], st["pieces_counted"], st.get("ms_merge", 0.0),
                      st["ms_count"], st["ms_partition"]))
     r = rows[-1]
     print(f"piece {arg} MB: ingest {r[0]:.2f} ms finish {r[1]:.2f} ms total {r[0] + r[1]:.2f} | h2d {r[2]:.2f} "

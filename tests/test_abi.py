@@ -32,7 +32,34 @@ def test_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert fk.lib().fk_abi_version() == 2
+    assert fk.lib().fk_abi_version() == 3 == fk.ABI_VERSION
+    with open(fk.HEADER_PATH) as f:
+        assert "#define FK_ABI_VERSION 3" in f.read()
+
+
+def _header_struct_fields(name: str) -> list[tuple[str, str]]:
+    import re
+    with open(fk.HEADER_PATH) as f:
+        text = f.read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), text, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    return re.findall(r"(int32_t|uint64_t|double)\s+(\w+);", body)
+
+
+@pytest.mark.parametrize("name,cls", [("fk_config", fk.fk_config), ("fk_stats", fk.fk_stats)])
+def test_ctypes_structs_mirror_the_header(name, cls):
+    """The ctypes mirrors of fk_config / fk_stats have the header's fields, in order, with its
+    types (a layout change bumps FK_ABI_VERSION, see the header's policy)."""
+    ctype = {"int32_t": ctypes.c_int32, "uint64_t": ctypes.c_uint64, "double": ctypes.c_double}
+    want = [(n, ctype[t]) for t, n in _header_struct_fields(name)]
+    assert want and [(n, t) for n, t in cls._fields_] == want
+
+
+def test_error_codes_mirror_the_header():
+    import re
+    with open(fk.HEADER_PATH) as f:
+        codes = {int(v): n for n, v in re.findall(r"#define (FK_E_\w+) \((-\d+)\)", f.read())}
+    assert codes == fk.ERRORS and codes[-7] == "FK_E_COMM"
 
 
 @pytest.mark.parametrize("kw,ok", [

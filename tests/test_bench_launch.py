@@ -49,3 +49,40 @@ def test_launcher_world_size_must_match():
     p = _run(["--gpus", "4", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2
     assert "WORLD_SIZE=2" in p.stderr
+
+
+def _fake_kfd(root, n_gpus, n_cpus=2):
+    """A KFD topology tree: CPU nodes (simd_count 0) first, then GPU nodes."""
+    for i in range(n_cpus + n_gpus):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        simd = 0 if i < n_cpus else 1024
+        (d / "properties").write_text(f"cpu_cores_count {0 if simd else 64}\nsimd_count {simd}\n"
+                                      f"location_id {i * 8}\ndomain 0\n")
+    (root / "not_a_node").mkdir()
+
+
+def test_gpu_count_from_sysfs(tmp_path, monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    _fake_kfd(tmp_path, 8)
+    for v in bench.VISIBILITY_VARS:
+        monkeypatch.delenv(v, raising=False)
+    assert len(bench.kfd_gpus(str(tmp_path))) == 8
+    assert bench.count_gpus(str(tmp_path)) == 8
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,3")
+    assert bench.count_gpus(str(tmp_path)) == 2
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")
+    assert bench.count_gpus(str(tmp_path)) == 1
+    assert bench.count_gpus(str(tmp_path / "missing")) == 0
+
+
+def test_launcher_counts_gpus_from_sysfs(tmp_path):
+    # the launcher process counts the devices from the KFD topology (no HIP call in the parent)
+    _fake_kfd(tmp_path, 4)
+    env = {"FASTKMER_KFD_TOPOLOGY": str(tmp_path)}
+    p = _run(["--gpus", "4", "--steps", "1", "--dry-run"], env)
+    assert p.returncode == 0, p.stderr
+    assert json.loads(p.stdout.strip().splitlines()[-1])["visible_gpus"] == 4
+    p = _run(["--gpus", "8", "--steps", "1"], env)
+    assert p.returncode == 2 and "only 4 GPU(s) visible" in p.stderr

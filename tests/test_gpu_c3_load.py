@@ -1,0 +1,179 @@
+"""BASELINE configs[2]'s real per-GPU load (k=28 m=10 x=3 B=8192, 6.25 GB of
+100 bp reads from a 3 Gbp virtual genome: one GPU's share of the 50 GB job)
+on the bench's own path, checked bin by bin (needs a GPU).
+
+The FASTA is made exactly as ``bench.Rank`` makes it (device generator, then
+staged to pinned host memory) and ingested exactly as ``bench.Rank.step_host``
+does (``fk_ingest`` from the pinned buffer: H2D segments, the fused map on
+every landed tile, staged pieces expanded while later bytes land, the heavy
+buckets split into sub-buckets, the large path) and counted by ``fk_finish``.
+
+* Both count modes against the C oracle (extractKXmers, SBKC:428-660, in
+  order; extractKXmersHT, SBKC:664-739, as sets) on every bin b with
+  b % 64 == r: the oracle walks the whole 6.25 GB (all k-mers counted) and
+  keeps 1/64 of the bins (``fko_count_mt_filtered``) so that it fits a test
+  run; r is the residue of the GPU's largest bin, where the heavy buckets
+  sit.
+* The same shard through one in-process exchange rank (the library's N > 1
+  path: pieces grouped by (owner, local bin), exchanged in steps, received
+  segments staged) against the same shard counted whole from HBM
+  (``fk_ingest_device``): every one of the 8192 bins, by a 128-bit digest of
+  its keys and of its counts.
+
+Run alone (``-s`` prints progress): each test takes ~1 minute on one MI355X.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import fastkmer_amd as fk
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+K, M, X, B = 28, 10, 3, 8192
+READ, GENOME, SEED = 100, 3_000_000_000, 0x5EED
+REC = READ + 14
+MOD = 64
+LOAD = int(float(os.environ.get("FASTKMER_C3_LOAD_GB", "6.25")) * 1e9)
+
+
+def _log(msg):
+    print(f"[c3-load {time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+@pytest.fixture(scope="module")
+def shard():
+    """bench.Rank's input for configs[2] (workload c3) on rank 0: generated on the device, staged to
+    pinned host memory."""
+    import torch
+    n_reads = LOAD // REC
+    nbytes = n_reads * REC
+    dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    fk.synth_fasta_to_device(dev.data_ptr(), n_reads, READ, GENOME, seed=SEED, first_read=0)
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dev)
+    torch.cuda.synchronize()
+    del dev
+    torch.cuda.empty_cache()
+    _log(f"shard: {nbytes} FASTA bytes in pinned host memory")
+    yield host, nbytes
+    del host
+
+
+@pytest.fixture(scope="module")
+def residue(shard):
+    """The residue class of bins the oracle keeps: that of the GPU's largest bin (sorted count)."""
+    host, nbytes = shard
+    with fk.KmerCounter(K, M, X, B) as kc:
+        kc.ingest_ptr(host.data_ptr(), nbytes)
+        kc.finish()
+        sizes = kc.bin_sizes()
+    return int(np.argmax(sizes)) % MOD
+
+
+@pytest.fixture(scope="module")
+def ref(shard, residue):
+    host, nbytes = shard
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    t0 = time.perf_counter()
+    r = oracle.OracleResult(None, K, M, B, threads=threads, bin_mod=MOD, bin_rem=residue, ptr=host.data_ptr(),
+                            nbytes=nbytes)
+    _log(f"oracle: {r.total_kmers} k-mers walked, bins b % {MOD} == {residue} kept "
+         f"({sum(r.bin_size(b) for b in range(residue, B, MOD))} distinct), {threads} threads, "
+         f"{time.perf_counter() - t0:.1f} s")
+    return r
+
+
+def _ascending(keys):
+    return bool(np.all(keys[1:] > keys[:-1]))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("use_ht", [False, True], ids=["sorted", "useHT"])
+def test_c3_load_pinned_staged_vs_oracle(shard, residue, ref, use_ht):
+    host, nbytes = shard
+    with fk.KmerCounter(K, M, X, B, use_ht) as kc:
+        for step in range(2):  # the second job reuses every buffer the first one grew (the bench's steady state)
+            t0 = time.perf_counter()
+            kc.ingest_ptr(host.data_ptr(), nbytes)
+            kc.finish()
+            _log(f"{'useHT' if use_ht else 'sorted'} step {step}: {(time.perf_counter() - t0) * 1e3:.1f} ms")
+        st = kc.stats()
+        sizes = kc.bin_sizes()
+        assert st["kmers"] == ref.total_kmers
+        assert int(sizes.sum()) == st["distinct"]
+        # the bench's own configuration at this load: staged pieces, the heavy-bucket split, the large path
+        assert st["pieces_counted"] >= 2
+        assert st["split_buckets"] >= 150_000 and st["sub_buckets"] > st["split_buckets"]
+        assert st["oversize_buckets"] >= 1
+        kept = list(range(residue, B, MOD))
+        n_keys = 0
+        for b in kept:
+            _, rlo, rcnt = ref.bin_arrays(b)
+            assert int(sizes[b]) == len(rlo), f"bin {b}: {int(sizes[b])} distinct, oracle {len(rlo)}"
+            keys, counts = kc.get_bin(b)
+            if use_ht:  # the hash count's order is its table's (fastutil's is unpinned): compare as sets
+                order = np.argsort(keys, kind="stable")
+                keys, counts = keys[order], counts[order]
+            else:
+                assert _ascending(keys), f"bin {b} not ascending"
+            assert np.array_equal(keys, rlo), f"bin {b}: keys differ from the oracle"
+            assert np.array_equal(counts, rcnt), f"bin {b}: counts differ from the oracle"
+            n_keys += len(rlo)
+        _log(f"{'useHT' if use_ht else 'sorted'}: {len(kept)} bins, {n_keys} distinct k-mers bit-exact; "
+             f"{st['distinct']} distinct in all, split buckets {st['split_buckets']} -> {st['sub_buckets']} "
+             f"sub-buckets, large-path buckets {st['oversize_buckets']}, pieces {st['pieces_counted']}")
+
+
+def _bin_digests(kc):
+    import xxhash
+    sizes = kc.bin_sizes()
+    out = []
+    for b in range(B):
+        if not sizes[b]:
+            out.append((0, None, None))
+            continue
+        keys, counts = kc.get_bin(b)
+        out.append((len(counts), xxhash.xxh3_128_hexdigest(keys), xxhash.xxh3_128_hexdigest(counts)))
+    return sizes, out
+
+
+@pytest.mark.timeout(900)
+def test_c3_load_exchange_rank_vs_whole_count(shard):
+    """One in-process exchange rank (bench.py --rehearse-local 1) against the shard counted whole from
+    HBM, every bin."""
+    import torch
+    host, nbytes = shard
+    dev = host.to("cuda")
+    with fk.KmerCounter(K, M, X, B) as kc:
+        kc.ingest_device(dev.data_ptr(), nbytes)
+        kc.finish()
+        torch.cuda.synchronize()
+        whole_st = kc.stats()
+        whole_sizes, whole = _bin_digests(kc)
+    del dev
+    torch.cuda.empty_cache()
+    _log(f"whole-input count from HBM: {whole_st['distinct']} distinct, digests of {B} bins")
+    kc = fk.KmerCounter(K, M, X, B, n_ranks=1, rank=0)
+    try:
+        fk.comm_init_local([kc])
+        for step in range(2):
+            t0 = time.perf_counter()
+            kc.ingest_ptr(host.data_ptr(), nbytes)
+            kc.finish()
+            _log(f"exchange rank step {step}: {(time.perf_counter() - t0) * 1e3:.1f} ms")
+        st = kc.stats()
+        assert kc.comm_transport == "local"
+        assert st["xch_steps"] >= 5 and st["pieces_counted"] >= 2
+        assert st["kmers"] == whole_st["kmers"] and st["distinct"] == whole_st["distinct"]
+        sizes, got = _bin_digests(kc)
+        assert np.array_equal(sizes, whole_sizes)
+        bad = [b for b in range(B) if got[b] != whole[b]]
+        assert not bad, f"{len(bad)} bins differ, first {bad[:8]}"
+        _log(f"exchange rank: all {B} bins identical to the whole-input count ({st['xch_steps']} steps, "
+             f"{st['pieces_counted']} staged pieces, split buckets {st['split_buckets']})")
+    finally:
+        kc.close()

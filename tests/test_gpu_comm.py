@@ -238,6 +238,60 @@ def test_rccl_single_rank_self_exchange(small_pieces):
             assert_union_matches_oracle([kc], ref)
 
 
+def test_rccl_single_rank_counts_on_the_records_communicator(small_pieces, monkeypatch):
+    # FASTKMER_COMM_SPLIT=0: the per-step counts on the records' communicator and the comm stream
+    # (no ncclCommSplit) -- the switch that rules the two-communicator ordering out on a first N-GPU run
+    import torch
+    monkeypatch.setenv("FASTKMER_COMM_SPLIT", "0")
+    fasta = fk.synth_fasta(30_000, 100, 600_000, seed=0xE7)
+    host = torch.empty(len(fasta), dtype=torch.uint8).pin_memory()
+    host.numpy()[:] = np.frombuffer(fasta, dtype=np.uint8)
+    with fk.KmerCounter(28, 10, 3, 2048, n_ranks=1, rank=0) as kc:
+        kc.comm_init(fk.comm_unique_id())
+        for _ in range(2):
+            kc.ingest_ptr(host.data_ptr(), len(fasta))
+            kc.finish()
+            assert kc.stats()["xch_steps"] >= 3
+            assert_union_matches_oracle([kc], oracle.OracleResult(fasta, 28, 10, 2048))
+        assert (kc.comm_allreduce(np.arange(5)) == np.arange(5)).all()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_rccl_wait_times_out_and_aborts(monkeypatch, split):
+    """A rank whose collective never completes (here: its streams held by a kernel spinning on a
+    host-mapped flag, as behind a dead peer) returns FK_E_COMM after FASTKMER_COMM_TIMEOUT_S instead
+    of blocking; the communicator is aborted and later collectives fail at once (the reference fails
+    the Spark job when a task fails, SBKC:1031-1043)."""
+    import time
+    monkeypatch.setenv("FASTKMER_COMM_TIMEOUT_S", "3")
+    monkeypatch.setenv("FASTKMER_COMM_SPLIT", split)
+    L = fk.lib()
+    kc = fk.KmerCounter(28, 10, 3, 2048, n_ranks=1, rank=0)
+    try:
+        kc.comm_init(fk.comm_unique_id())
+        assert (kc.comm_allreduce(np.array([3, 4])) == [3, 4]).all()  # healthy first
+        assert L.fk_debug_comm_hold(kc._h, 30) == 0
+        # released well after the timeout: the abort may wait for the held kernel to end
+        timer = threading.Timer(6.0, lambda: L.fk_debug_comm_release(kc._h))
+        timer.start()
+        t0 = time.perf_counter()
+        with pytest.raises(fk.FastKmerError) as e:
+            kc.comm_allreduce(np.array([1, 2, 3]))
+        dt = time.perf_counter() - t0
+        timer.join()
+        assert e.value.code == -7 and "timed out after 3 s" in str(e.value), e.value
+        assert 3.0 <= dt < 25.0
+        t0 = time.perf_counter()
+        with pytest.raises(fk.FastKmerError) as e2:  # the communicator is gone: fail fast
+            kc.comm_allreduce(np.array([1]))
+        assert e2.value.code == -7 and "aborted" in str(e2.value)
+        assert time.perf_counter() - t0 < 1.0
+    finally:
+        L.fk_debug_comm_release(kc._h)
+        kc.close()
+
+
 def _rccl_rank(rank, world, uid, path, out_dir, q):
     try:
         import torch  # noqa: F401  (one HIP runtime per process, see fastkmer_amd.lib)

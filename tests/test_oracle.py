@@ -166,6 +166,28 @@ def test_oracle_threads_match_single(threads):
             assert a.all_dict() == b.all_dict()
 
 
+@pytest.mark.parametrize("mod,rem", [(1, 0), (4, 3), (64, 17)])
+def test_oracle_bin_filter_keeps_exactly_its_bins(mod, rem):
+    # fko_count_mt_filtered (the checker of the configs[2] per-GPU load): the kept bins are the
+    # unfiltered oracle's, every other bin is empty, and every k-mer is still walked and counted
+    import ctypes
+    import fastkmer_amd as fk
+    fa = fk.synth_fasta(4000, 100, 300_000, seed=5)
+    full = oracle.OracleResult(fa, 28, 10, 2048)
+    buf = ctypes.create_string_buffer(fa, len(fa))
+    for threads in (1, 3):
+        f = oracle.OracleResult(None, 28, 10, 2048, threads=threads, bin_mod=mod, bin_rem=rem,
+                                ptr=ctypes.addressof(buf), nbytes=len(fa))
+        assert (f.total_kmers, f.superkmers, f.reads) == (full.total_kmers, full.superkmers, full.reads)
+        for b in range(2048):
+            if b % mod == rem:
+                assert all((x == y).all() for x, y in zip(f.bin_arrays(b), full.bin_arrays(b))), b
+            else:
+                assert f.bin_size(b) == 0
+    with pytest.raises(ValueError):
+        oracle.OracleResult(fa, 28, 10, 2048, bin_mod=4, bin_rem=4)
+
+
 # ---------------------------------------------------------------- bin-signature diagnostics
 
 def _binsig_files(counts, m, B, tmp_path):
