@@ -2405,9 +2405,13 @@ static int note_held(fk_ctx *c, int rc) {
     FK_HELD(flags); FK_HELD(flag_scan); FK_HELD(cell_total); FK_HELD(cell_base); FK_HELD(dense_keys);
     FK_HELD(dense_counts); FK_HELD(bucket_unique);
     FK_HELD(sp_keys); FK_HELD(sp_subs); FK_HELD(xsend); FK_HELD(xrecv);
-    FK_HELD(gather_keys); FK_HELD(st_keys[0]); FK_HELD(st_keys[1]); FK_HELD(st_keys[2]); FK_HELD(st_keys[3]);
-    FK_HELD(part.K); FK_HELD(part.KT); FK_HELD(dest.K); FK_HELD(dest.KT);
+    FK_HELD(gather_keys); FK_HELD(part.K); FK_HELD(part.KT); FK_HELD(dest.K); FK_HELD(dest.KT);
 #undef FK_HELD
+    std::vector<std::string> piece_names(STAGE_MAXP);
+    for (int p = 0; p < STAGE_MAXP; ++p) {
+        piece_names[p] = "st_keys[" + std::to_string(p) + "]";
+        add(piece_names[p].c_str(), c->st_keys[p]);
+    }
     std::sort(v.rbegin(), v.rend());
     size_t total = 0;
     for (const auto &e : v) total += e.first;
@@ -2896,11 +2900,16 @@ static int split_sample(const char *path, int32_t world, int32_t rank, int32_t k
             // the block's first line is dropped (it may be the tail of a header line: the block
             // started inside it, or the file's first header), and the block ends at the next
             // header line (a later record's name is not sequence)
+            // -- unless the block holds no newline at all: it lies inside one sequence line (an unwrapped
+            // record), and the whole block is sequence (a header line of a megabyte is not a FASTA)
             size_t a = 0;
             while (a < buf.size() && buf[a] != '\n') ++a;
-            a = a < buf.size() ? a + 1 : buf.size();
+            if (a == buf.size())
+                a = (at == 0 && !buf.empty() && buf[0] == '>') ? buf.size() : 0;
+            else
+                a += 1;
             size_t e = a;
-            while (e < buf.size() && !(buf[e] == '>' && buf[e - 1] == '\n')) ++e;
+            while (e < buf.size() && !(buf[e] == '>' && e > 0 && buf[e - 1] == '\n')) ++e;
             if (e <= a) continue;
             const uint8_t h[3] = {'\n', '>', '\n'};
             out.insert(out.end(), h, h + 3);

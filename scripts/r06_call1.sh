@@ -9,6 +9,10 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_comm.py -v --timeout 200 --
   -p no:cacheprovider > $O/comm.log 2>&1
 rc=$?; tail -3 $O/comm.log; grep -E "FAILED|ERROR" $O/comm.log | head -20
 [[ $rc -gt 1 ]] && { echo "comm rc=$rc"; tail -30 $O/comm.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_wave.py tests/test_gpu_parity.py -v --timeout 200 --timeout-method thread \
+  -p no:cacheprovider > $O/wave_parity.log 2>&1
+rc=$?; tail -3 $O/wave_parity.log; grep -E "FAILED|ERROR" $O/wave_parity.log | head -20
+[[ $rc -gt 1 ]] && { echo "wave/parity rc=$rc"; tail -30 $O/wave_parity.log; exit 1; }
 timeout -k 10 900 python -u -m pytest tests/test_gpu_c3_load.py -v -s --timeout 900 --timeout-method thread \
   -p no:cacheprovider > $O/c3_load.log 2>&1
 rc=$?; grep -E "c3-load|passed|failed|FAILED|Error" $O/c3_load.log | tail -20

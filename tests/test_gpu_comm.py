@@ -449,6 +449,36 @@ def test_local_exchange_size_aware_placement(small_pieces, tmp_path, use_ht, k, 
     assert lpt <= default * 1.02, (lpt, default)
 
 
+def test_size_aware_placement_single_line_long_record(small_pieces, tmp_path):
+    # a long record whose sequence is one unwrapped line (sequenceType=1) -- every 1 MB
+    # sample block lies inside that line and is all sequence; the sample must not come back empty
+    # (the placement would silently stay bin % n)
+    G = 2
+    rng = np.random.default_rng(0x5A)
+    seq = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 12_000_000)].tobytes()
+    fasta = b">chrOneLine\n" + seq + b"\n"
+    path = tmp_path / "one_line.fa"
+    path.write_bytes(fasta)
+    ctxs = [fk.KmerCounter(28, 10, 3, 2048, sequence_type=1, n_ranks=G, rank=r) for r in range(G)]
+    fk.comm_init_local(ctxs)
+    owners, errs = [None] * G, [None] * G
+
+    def work(r):
+        try:
+            owners[r] = ctxs[r].balance_bins_file(str(path), fraction=0.25)
+            ctxs[r].ingest_file_range(str(path))
+            ctxs[r].finish()
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+    th = [threading.Thread(target=work, args=(r,)) for r in range(G)]
+    [t.start() for t in th]
+    [t.join(timeout=300) for t in th]
+    assert errs == [None] * G, errs
+    assert np.array_equal(owners[0], owners[1])
+    assert not np.array_equal(owners[0], np.arange(2048) % G), "empty sample: the placement stayed bin % n"
+    assert_union_matches_oracle(ctxs, oracle.OracleResult(fasta, 28, 10, 2048, sequence_type=1), owner=owners[0])
+
+
 def test_local_exchange_rank_closed_right_after_finish(small_pieces):
     # a rank destroyed right after fk_finish while its peer may still be in the job's
     # last step (waiting on the closed rank's events, copying out of its send buffer) -- the peer's
