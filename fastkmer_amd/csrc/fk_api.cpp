@@ -1638,6 +1638,21 @@ static CountBufs main_bufs(fk_ctx *c) {
                      &c->out_counts};
 }
 
+// The listed buckets of at most cap keys above skip_le keys (skip_le: counted by a mid wave tier) in one
+// workgroup's LDS: the block kernel (64-bit keys) or the LDS radix sort (128-bit keys).
+static int block_tier(fk_ctx *c, const BucketSrc &src, CountBufs B, DevBuf &okb, const uint32_t *list, uint32_t n,
+                      uint32_t cap, uint32_t skip_le, hipStream_t s) {
+    if (c->KW == 1)
+        HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), n, c->cfg.k, okb.as<uint64_t>(),
+                                      B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                      c->misc.as<unsigned long long>() + 1, cap, 99, list, s, skip_le));
+    else
+        HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), n, c->cfg.k, okb.as<uint64_t>(),
+                                   B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
+                                   c->misc.as<unsigned long long>() + 1, cap, list, s, skip_le));
+    return FK_OK;
+}
+
 // 4c + 5: buckets over cell_total / cell_base (ncell_all cells), their exact counts from `src` (one
 // key array, or the staged pieces') into okb / B.out_counts at each bucket's first slot, the
 // distinct keys per bucket in B.bucket_unique; *nb_out = buckets
@@ -1699,7 +1714,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         // the block tier's top: 64-bit keys with the split, the mid wave tier's cap (above it: split)
         // (the 513..1024-key buckets through the split as well, no mid wave tier: configs[2] load
         // 1.1-1.4 ms slower, configs[1] 0.3 ms, profiles/r05zg_mid_split_ab.txt)
-        const uint32_t block_top = (c->KW == 1 && FK_SPLIT_HEAVY) ? WAVE_MID_CAP : cap;
+        const uint32_t block_top = FK_SPLIT_HEAVY ? (c->KW == 1 ? WAVE_MID_CAP : WAVE128_MID_CAP) : cap;
         HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, block_top,
                                     B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(),
                                     c->misc.as<unsigned long long>() + 3, s));
@@ -1725,24 +1740,27 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         htrace("sorted: tiers read");
         c->stats.block_buckets = ntier[0];
         c->stats.big_buckets = ntier[1];
-        hipStream_t ts = s;
         uint64_t nlarge = 0;
-        if (c->KW == 1 && (ntier[0] || ntier[1])) {
-            // 64-bit keys above the wave tier.  The block tier (513 .. WAVE_MID_CAP keys) is counted by
-            // the mid wave tier, one wave per bucket.  The big tier (above it) is split into wave-sized
-            // sub-buckets by sampled splitters, counted by the wave tier and joined back; a bucket with a
-            // sub-bucket too large for a wave (a k-mer repeated that often) falls back to the block
-            // kernel (<= cap keys) or the big-table kernel.  Without the split (-DFK_SPLIT_HEAVY=0, A/B
-            // builds) the block tier reaches cap and the block kernel takes its buckets above WAVE_MID_CAP.
+        if (ntier[0] || ntier[1]) {
+            // Above the wave tier.  The block tier (up to the mid wave tier's cap: 1024 keys for 64-bit
+            // keys, 512 for 128-bit ones) is counted by the mid wave tier, one wave per bucket.  The big
+            // tier (above it) is split into wave-sized sub-buckets by sampled splitters and counted in
+            // order by one wave per bucket; a bucket with a sub-bucket too large for a wave (a k-mer
+            // repeated that often) falls back to the block kernel / LDS sort (<= cap keys) or the
+            // big-table kernel (64-bit) and the streaming path.  Without the split (-DFK_SPLIT_HEAVY=0,
+            // A/B builds) the block tier reaches cap and the block kernel / LDS sort takes its buckets
+            // above the mid wave tier's cap.
+            const bool w1 = c->KW == 1;
             const uint32_t *l1 = lists + nbuckets;
-            uint32_t *fbB = nullptr, *fbG = lists + nbuckets;  // the block / big-table kernels' lists
+            uint32_t *fbB = nullptr, *fbG = lists + nbuckets;  // the fallback lists (block / big)
             uint32_t nfbB = 0, nfbG = ntier[1];
             if (FK_SPLIT_HEAVY && ntier[1]) {  // nothing to split: no split kernels, no read-back
                 const uint32_t nl = ntier[1];
                 const uint64_t maxsub = listed_keys / 64 + nl + 64;  // >= ceil(n / SPL_TGT) sub-buckets per bucket
+                const size_t sub_bytes = w1 ? sizeof(SubBucket) : sizeof(SubBucket128);
                 FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
-                FK_TRY(ensure(c->sp_keys, listed_keys * 8));
-                FK_TRY(ensure(c->sp_subs, maxsub * sizeof(SubBucket)));
+                FK_TRY(ensure(c->sp_keys, listed_keys * 8 * c->KW));
+                FK_TRY(ensure(c->sp_subs, maxsub * sub_bytes));
                 FK_TRY(ensure(c->sp_par, (uint64_t)nl * sizeof(SplitParent)));
                 FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
                 uint32_t *fb = c->sp_fb.as<uint32_t>();
@@ -1750,9 +1768,15 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(), s));
                 HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
                                           c->sp_base.as<uint64_t>() + nl, c->ws, s));
-                HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(),
-                                              c->sp_keys.as<uint64_t>(), c->sp_subs.as<SubBucket>(),
-                                              c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, s));
+                if (w1)
+                    HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, 0, l1, nl,
+                                                  c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
+                                                  c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb,
+                                                  fb + nl, cap, k, F, s));
+                else
+                    HIP_TRY(launch_bucket_split128(src, B.buckets->as<Bucket>(), l1, nl, c->sp_base.as<uint64_t>(),
+                                                   c->sp_keys.as<uint64_t>(), c->sp_subs.as<SubBucket128>(),
+                                                   c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, s));
                 HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipEventRecord(c->tier_ev, s));
                 HIP_TRY(hipEventSynchronize(c->tier_ev));
@@ -1761,7 +1785,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 fbB = fb, nfbB = sc[1], fbG = fb + nl, nfbG = sc[2];
                 htrace("sorted: split counts read");
 #ifdef FK_PROBES
-                if (getenv("FASTKMER_HOST_TRACE")) {  // the split buckets by size class: buckets, keys, fallbacks
+                if (w1 && getenv("FASTKMER_HOST_TRACE")) {  // the split buckets by size class: buckets, keys, fallbacks
                     std::vector<uint64_t> base((size_t)nl + 1);
                     std::vector<uint32_t> f(2 * (size_t)nl), h_l((size_t)nl);
                     HIP_TRY(hipMemcpy(base.data(), c->sp_base.p, base.size() * 8, hipMemcpyDeviceToHost));
@@ -1795,34 +1819,42 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
 #endif
                 if (nsub > maxsub) return set_err(FK_E_DEVICE, "bucket split: %u sub-buckets of at most %llu", nsub,
                                                   (unsigned long long)maxsub);
-                HIP_TRY(launch_sub_count64_seq(B.buckets->as<Bucket>(), l1, nl, c->sp_par.as<SplitParent>(),
-                                               c->sp_subs.as<SubBucket>(), c->sp_keys.as<uint64_t>(), okb.as<uint64_t>(),
-                                               B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(), s,
-                                               ordered));
+                if (w1)
+                    HIP_TRY(launch_sub_count64_seq(B.buckets->as<Bucket>(), l1, nl, c->sp_par.as<SplitParent>(),
+                                                   c->sp_subs.as<SubBucket>(), c->sp_keys.as<uint64_t>(),
+                                                   okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                   B.bucket_unique->as<uint64_t>(), s, ordered));
+                else
+                    HIP_TRY(launch_sub_count128_seq(B.buckets->as<Bucket>(), l1, nl, c->sp_par.as<SplitParent>(),
+                                                    c->sp_subs.as<SubBucket128>(), c->sp_keys.as<uint64_t>(),
+                                                    okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                    B.bucket_unique->as<uint64_t>(), s, ordered));
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
+            const uint32_t mid_cap = w1 ? WAVE_MID_CAP : WAVE128_MID_CAP;
             if (ntier[0]) {
-                HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
-                                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                       B.bucket_unique->as<uint64_t>(), s, ordered));
-                if (block_top > WAVE_MID_CAP)  // no split: the block tier's buckets above the mid wave tier
-                    HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), ntier[0], k, okb.as<uint64_t>(),
-                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                  c->misc.as<unsigned long long>() + 1, cap, 99, lists, s,
-                                                  WAVE_MID_CAP));
+                if (w1)
+                    HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                           okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                           B.bucket_unique->as<uint64_t>(), s, ordered));
+                else
+                    HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                            okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                            B.bucket_unique->as<uint64_t>(), s, ordered));
+                if (block_top > mid_cap)  // no split: the block tier's buckets above the mid wave tier
+                    FK_TRY(block_tier(c, src, B, okb, lists, ntier[0], cap, mid_cap, s));
             }
-            if (nfbB)
-                HIP_TRY(launch_bucket_count64(src, B.buckets->as<Bucket>(), nfbB, k, okb.as<uint64_t>(),
-                                              B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                              c->misc.as<unsigned long long>() + 1, cap, 99, fbB, s));
-            if (nfbG) {
+            if (nfbB) FK_TRY(block_tier(c, src, B, okb, fbB, nfbB, cap, 0, s));
+            if (nfbG && w1) {
                 // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
                 HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfbG, k, okb.as<uint64_t>(),
                                                   B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
                                                   c->misc.as<unsigned long long>() + 2, fbG, s));
                 HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
+            } else if (nfbG) {
+                nlarge = nfbG;  // 128-bit keys: no big-table kernel
             }
             if (nlarge) {  // scratch for the listed buckets' keys only, taken by a cursor
                 FK_TRY(ensure(c->scratch, listed_keys * 8 * c->KW));
@@ -1831,26 +1863,6 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                                  c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
                                                  fbG, s, c->misc.as<unsigned long long>() + 6));
-            }
-        } else if (ntier[0] || ntier[1]) {
-            // 128-bit keys: the block-tier buckets of at most WAVE128_MID_CAP keys take a wave with a
-            // 768-slot table (a cell of a large bin, ~340 keys at configs[3]'s per-GPU bins), the rest
-            // the LDS radix sort; buckets above the block tier the streaming path
-            HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
-                                                    okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                    B.bucket_unique->as<uint64_t>(), ts, ordered));
-            HIP_TRY(launch_bucket_sort(2, src, B.buckets->as<Bucket>(), ntier[0], k,
-                                       okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                       B.bucket_unique->as<uint64_t>(), c->misc.as<unsigned long long>() + 1, cap,
-                                       lists, ts, WAVE128_MID_CAP));
-            nlarge = ntier[1];
-            if (nlarge) {  // scratch for the listed buckets' keys only, taken by a cursor
-                FK_TRY(ensure(c->scratch, listed_keys * 8 * c->KW));
-                HIP_TRY(hipMemsetAsync(c->misc.as<unsigned long long>() + 6, 0, 8, ts));
-                HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), ntier[1], k,
-                                                 c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
-                                                 B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                 lists + nbuckets, ts, c->misc.as<unsigned long long>() + 6));
             }
         }
         c->stats.oversize_buckets = nlarge;
@@ -3029,13 +3041,23 @@ FK_EXPORT int fk_debug_comm_hold(fk_ctx *c, int32_t max_seconds) {
     __atomic_store_n(c->hold_flag, 0u, __ATOMIC_RELEASE);
     void *dflag = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dflag, c->hold_flag, 0));
+    // wall-clock ticks of max_seconds: the attribute is in kHz (100 MHz on gfx950); a rate reported
+    // below that bounds the hold by 100 MHz ticks instead (longer, never shorter, than asked)
     int khz = 0;
     HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
-    const uint64_t ticks = (uint64_t)max_seconds * (uint64_t)std::max(khz, 1) * 1000ull;
+    const uint64_t ticks = (uint64_t)max_seconds * (uint64_t)std::max(khz, 100000) * 1000ull;
     const hipStream_t cs2 = c->comm->counts_stream();
     for (hipStream_t st : {c->comm_stream, cs2})
         if (st) HIP_TRY(launch_hold_stream(static_cast<const uint32_t *>(dflag), ticks, st));
     return FK_OK;
+}
+
+FK_EXPORT int fk_debug_comm_held(fk_ctx *c) {
+    if (!c || !c->comm_stream) return 0;
+    DeviceGuard dg_(c->device);
+    const hipError_t e = hipStreamQuery(c->comm_stream);
+    if (e != hipErrorNotReady) (void)hipGetLastError();
+    return e == hipErrorNotReady ? 1 : 0;
 }
 
 FK_EXPORT int fk_debug_comm_release(fk_ctx *c) {

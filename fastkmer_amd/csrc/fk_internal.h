@@ -263,6 +263,20 @@ hipError_t launch_bucket_split64(const BucketSrc &src, const Bucket *buckets, co
 hipError_t launch_sub_count64_seq(const Bucket *buckets, const uint32_t *list, uint32_t nl, const SplitParent *parents,
                                   const SubBucket *subs, const uint64_t *skeys, uint64_t *out_keys,
                                   uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s, bool ordered);
+// the same for 128-bit keys (33 <= k <= 63): sub-bucket keys as (hi, lo) word pairs, counted by the mid
+// wave tier's 512-key table; fallbacks: fb0 (<= block_cap keys, the LDS sort), fb1 (the streaming path)
+struct SubBucket128 {
+    uint64_t src;          // first key (pair index) in the split copy
+    uint64_t lo_hi, lo_lo; // every key lies in [lo, lo + 2^span)
+    uint32_t n, span;
+};
+hipError_t launch_bucket_split128(const BucketSrc &src, const Bucket *buckets, const uint32_t *list, uint32_t nl,
+                                  const uint64_t *sbase, uint64_t *skeys, SubBucket128 *subs, SplitParent *parents,
+                                  unsigned int *counts, uint32_t *fb0, uint32_t *fb1, uint32_t block_cap, int k, int F,
+                                  hipStream_t s);
+hipError_t launch_sub_count128_seq(const Bucket *buckets, const uint32_t *list, uint32_t nl, const SplitParent *parents,
+                                   const SubBucket128 *subs, const uint64_t *skeys, uint64_t *out_keys,
+                                   uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s, bool ordered);
 // dst[i] += src[i] (dst = src when `copy`)
 hipError_t launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n, bool copy, hipStream_t s);
 // skip_le: listed buckets of at most this many keys were counted by a wave tier (skipped)

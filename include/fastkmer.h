@@ -29,7 +29,7 @@ extern "C" {
  * (fk_config, fk_stats) or an error code's meaning changes; callers compare
  * fk_abi_version() with the FK_ABI_VERSION they were built against.
  *   3: fk_stats lost four always-zero fields (ht_spilled, ht_rounds, ms_merge,
- *      ht_big_groups); FK_E_COMM; fk_debug_comm_hold / fk_debug_comm_release. */
+ *      ht_big_groups); FK_E_COMM; fk_debug_comm_hold / _release / _held. */
 #define FK_ABI_VERSION 3
 
 #define FK_OK 0
@@ -311,6 +311,8 @@ int fk_debug_wave_count(int32_t device, int32_t k, int32_t F, uint32_t c0, uint3
  * fk_destroy releases it too. */
 int fk_debug_comm_hold(fk_ctx *ctx, int32_t max_seconds);
 int fk_debug_comm_release(fk_ctx *ctx);
+/* 1 while the context's comm stream has not drained (e.g. still held), else 0. */
+int fk_debug_comm_held(fk_ctx *ctx);
 
 /* Measurement hook: per-phase wave cycles of the fused map kernel summed over
  * its launches since the last reset (out[0..16)); only a library built with

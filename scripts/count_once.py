@@ -5,7 +5,7 @@ import torch  # noqa
 import fastkmer_amd as fk
 kc = fk.KmerCounter(28, 10, 3, int(os.environ.get('FK_B', '2048')), use_ht=os.environ.get('FK_HT', '0') == '1')
 kc.synth_device(int(os.environ.get('FK_BYTES', '1000000000')) // 114, 100, int(os.environ.get('FK_GENOME', '100000000')), seed=0x5EED)
-for i in range(3):
+for i in range(int(os.environ.get('FK_JOBS', '3'))):
     kc.finish()
 st = kc.stats()
 print(f"count {st['ms_count']:.2f} ms  partition {st['ms_partition']:.2f}  buckets {st['buckets']} F {st['fine_bits']} "

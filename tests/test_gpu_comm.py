@@ -272,6 +272,8 @@ def test_rccl_wait_times_out_and_aborts(monkeypatch, split):
         kc.comm_init(fk.comm_unique_id())
         assert (kc.comm_allreduce(np.array([3, 4])) == [3, 4]).all()  # healthy first
         assert L.fk_debug_comm_hold(kc._h, 30) == 0
+        time.sleep(0.5)
+        assert L.fk_debug_comm_held(kc._h) == 1, "the hold kernel did not hold the comm stream"
         # released well after the timeout: the abort may wait for the held kernel to end
         timer = threading.Timer(6.0, lambda: L.fk_debug_comm_release(kc._h))
         timer.start()
