@@ -148,6 +148,7 @@ def lib():
         "fk_debug_comm_hold": (ctypes.c_int, [P, I32]),
         "fk_debug_comm_release": (ctypes.c_int, [P]),
         "fk_debug_comm_held": (ctypes.c_int, [P]),
+        "fk_debug_fingerprint_bits": (ctypes.c_int, [I32, I32]),
         "fk_debug_wave_count": (ctypes.c_int, [I32, I32, I32, ctypes.c_uint32, ctypes.c_uint32, I32, P,
                                                ctypes.c_uint32, P, P, P]),
     }

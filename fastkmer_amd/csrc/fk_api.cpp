@@ -3052,6 +3052,12 @@ FK_EXPORT int fk_debug_comm_hold(fk_ctx *c, int32_t max_seconds) {
     return FK_OK;
 }
 
+FK_EXPORT int fk_debug_fingerprint_bits(int32_t device, int32_t bits) {
+    DeviceGuard dg_(device);
+    HIP_TRY(set_fingerprint_bits(bits));
+    return FK_OK;
+}
+
 FK_EXPORT int fk_debug_comm_held(fk_ctx *c) {
     if (!c || !c->comm_stream) return 0;
     DeviceGuard dg_(c->device);

@@ -135,6 +135,7 @@ class RcclComm : public Comm {
     ~RcclComm() override {
         if (cstream_) (void)hipStreamSynchronize(cstream_);
         if (stage_) (void)hipFree(stage_);
+        if (hstage_) (void)hipHostFree(hstage_);
         if (cstream_) (void)hipStreamDestroy(cstream_);
         if (ccomm_) (void)api_->CommDestroy(ccomm_);
         if (comm_) (void)api_->CommDestroy(comm_);
@@ -159,15 +160,19 @@ class RcclComm : public Comm {
         const size_t bytes = (size_t)n_ * n * 8;
         if (stage(2 * bytes, s, err)) return -1;
         uint64_t *din = static_cast<uint64_t *>(stage_), *dout = din + (size_t)n_ * n;
-        COMM_HIP(hipMemcpyAsync(din, in, bytes, hipMemcpyHostToDevice, s));
+        uint64_t *hin = static_cast<uint64_t *>(hstage_), *hout = hin + (size_t)n_ * n;
+        memcpy(hin, in, bytes);  // pinned: the copies below never block the host (the wait is bounded)
+        COMM_HIP(hipMemcpyAsync(din, hin, bytes, hipMemcpyHostToDevice, s));
         if (nccl(api_->GroupStart(), err)) return -1;
         for (int p = 0; p < n_; ++p) {
             if (nccl(api_->Send(din + (size_t)p * n, n, ncclUint64, p, cm, s), err)) return end_group(err);
             if (nccl(api_->Recv(dout + (size_t)p * n, n, ncclUint64, p, cm, s), err)) return end_group(err);
         }
         if (nccl(api_->GroupEnd(), err)) return -1;
-        COMM_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s));
-        return wait(s, err);
+        COMM_HIP(hipMemcpyAsync(hout, dout, bytes, hipMemcpyDeviceToHost, s));
+        if (wait(s, err)) return -1;
+        memcpy(out, hout, bytes);
+        return 0;
     }
 
     int allreduce_sum_u64(uint64_t *v, size_t n, hipStream_t s, std::string &err) override {
@@ -176,10 +181,13 @@ class RcclComm : public Comm {
         ncclComm_t cm = ccomm_ ? ccomm_ : comm_;
         if (cstream_) s = cstream_;
         if (stage(n * 8, s, err)) return -1;
-        COMM_HIP(hipMemcpyAsync(stage_, v, n * 8, hipMemcpyHostToDevice, s));
+        memcpy(hstage_, v, n * 8);
+        COMM_HIP(hipMemcpyAsync(stage_, hstage_, n * 8, hipMemcpyHostToDevice, s));
         if (nccl(api_->AllReduce(stage_, stage_, n, ncclUint64, ncclSum, cm, s), err)) return -1;
-        COMM_HIP(hipMemcpyAsync(v, stage_, n * 8, hipMemcpyDeviceToHost, s));
-        return wait(s, err);
+        COMM_HIP(hipMemcpyAsync(hstage_, stage_, n * 8, hipMemcpyDeviceToHost, s));
+        if (wait(s, err)) return -1;
+        memcpy(v, hstage_, n * 8);
+        return 0;
     }
 
     int alltoallv(const uint8_t *send, const uint64_t *soff, const uint64_t *sbytes, uint8_t *recv,
@@ -283,15 +291,18 @@ class RcclComm : public Comm {
             if (el > 0.002) usleep(50);
         }
     }
-    // the staging buffer of the small collectives; the stream that last used it has drained (every
-    // collective ends in a wait on it), so it can be replaced
+    // the device and pinned host staging buffers of the small collectives (pageable host memory would
+    // make hipMemcpyAsync wait for the stream on the host, outside the bounded wait); the stream that
+    // last used them has drained (every collective ends in a wait on it), so they can be replaced
     int stage(size_t bytes, hipStream_t s, std::string &err) {
         (void)s;
         if (stage_bytes_ >= bytes) return 0;
         if (stage_) (void)hipFree(stage_);
-        stage_ = nullptr;
+        if (hstage_) (void)hipHostFree(hstage_);
+        stage_ = hstage_ = nullptr;
         stage_bytes_ = 0;
         COMM_HIP(hipMalloc(&stage_, bytes));
+        COMM_HIP(hipHostMalloc(&hstage_, bytes, hipHostMallocDefault));
         stage_bytes_ = bytes;
         return 0;
     }
@@ -299,7 +310,7 @@ class RcclComm : public Comm {
     ncclComm_t comm_;
     ncclComm_t ccomm_ = nullptr;    // the counts' communicator (split off comm_)
     hipStream_t cstream_ = nullptr; // ... and its stream
-    void *stage_ = nullptr;
+    void *stage_ = nullptr, *hstage_ = nullptr;
     size_t stage_bytes_ = 0;
     double timeout_s_;
     bool aborted_ = false;

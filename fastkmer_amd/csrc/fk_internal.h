@@ -300,6 +300,9 @@ hipError_t launch_bucket_compact(int KW, const uint64_t *out_keys, const uint32_
 hipError_t launch_bin_offsets(const uint64_t *flag_scan, const uint64_t *dense_off, uint32_t nlbins, int F,
                               uint64_t nbuckets, uint64_t *bin_off, hipStream_t s);
 
+// ---- test hook: the 128-bit wave tier's fingerprints cut to `bits` low bits (0: whole), current device
+hipError_t set_fingerprint_bits(int bits);
+
 // ---- test hook: a one-thread kernel holding stream s until *flag != 0 (host-mapped) or max_ticks
 // of the wall clock have passed
 hipError_t launch_hold_stream(const uint32_t *flag, uint64_t max_ticks, hipStream_t s);

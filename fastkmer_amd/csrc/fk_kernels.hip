@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include <limits>
+#include <type_traits>
 
 #include "fk_internal.h"
 

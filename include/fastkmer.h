@@ -29,7 +29,8 @@ extern "C" {
  * (fk_config, fk_stats) or an error code's meaning changes; callers compare
  * fk_abi_version() with the FK_ABI_VERSION they were built against.
  *   3: fk_stats lost four always-zero fields (ht_spilled, ht_rounds, ms_merge,
- *      ht_big_groups); FK_E_COMM; fk_debug_comm_hold / _release / _held. */
+ *      ht_big_groups); FK_E_COMM; fk_debug_comm_hold / _release / _held;
+ *      fk_debug_fingerprint_bits. */
 #define FK_ABI_VERSION 3
 
 #define FK_OK 0
@@ -313,6 +314,13 @@ int fk_debug_comm_hold(fk_ctx *ctx, int32_t max_seconds);
 int fk_debug_comm_release(fk_ctx *ctx);
 /* 1 while the context's comm stream has not drained (e.g. still held), else 0. */
 int fk_debug_comm_held(fk_ctx *ctx);
+
+/* Test hook: the 128-bit wave tier (33 <= k <= 63) dedupes on 64-bit key
+ * fingerprints and checks every key against its slot's claimer; a shared
+ * fingerprint sends the bucket to an exact count from registers.  This cuts
+ * the fingerprints of `device` to their low `bits` bits (0: whole, the
+ * product), so that tests drive that path on every bucket. */
+int fk_debug_fingerprint_bits(int32_t device, int32_t bits);
 
 /* Measurement hook: per-phase wave cycles of the fused map kernel summed over
  * its launches since the last reset (out[0..16)); only a library built with
