@@ -25,6 +25,20 @@ std::string hip_msg(const char *what, hipError_t e) {
     return std::string(what) + ": " + hipGetErrorString(e);
 }
 
+// dst[i] = src[i]: the small collectives' staging copies between pinned (mapped) host memory and the
+// device, as kernels on the collective's stream -- a small hipMemcpyAsync may be carried out by the
+// host once the stream has drained, which would block the host outside the bounded wait
+__global__ void k_comm_copy_u64(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+hipError_t comm_copy(uint64_t *dst, const uint64_t *src, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    k_comm_copy_u64<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, src, n);
+    return hipGetLastError();
+}
+
 #define COMM_HIP(expr)                                \
     do {                                              \
         hipError_t e_ = (expr);                       \
@@ -161,15 +175,16 @@ class RcclComm : public Comm {
         if (stage(2 * bytes, s, err)) return -1;
         uint64_t *din = static_cast<uint64_t *>(stage_), *dout = din + (size_t)n_ * n;
         uint64_t *hin = static_cast<uint64_t *>(hstage_), *hout = hin + (size_t)n_ * n;
-        memcpy(hin, in, bytes);  // pinned: the copies below never block the host (the wait is bounded)
-        COMM_HIP(hipMemcpyAsync(din, hin, bytes, hipMemcpyHostToDevice, s));
+        uint64_t *hin_d = static_cast<uint64_t *>(hstage_dev_), *hout_d = hin_d + (size_t)n_ * n;
+        memcpy(hin, in, bytes);  // mapped pinned memory, copied by kernels: nothing below blocks the host
+        COMM_HIP(comm_copy(din, hin_d, (size_t)n_ * n, s));
         if (nccl(api_->GroupStart(), err)) return -1;
         for (int p = 0; p < n_; ++p) {
             if (nccl(api_->Send(din + (size_t)p * n, n, ncclUint64, p, cm, s), err)) return end_group(err);
             if (nccl(api_->Recv(dout + (size_t)p * n, n, ncclUint64, p, cm, s), err)) return end_group(err);
         }
         if (nccl(api_->GroupEnd(), err)) return -1;
-        COMM_HIP(hipMemcpyAsync(hout, dout, bytes, hipMemcpyDeviceToHost, s));
+        COMM_HIP(comm_copy(hout_d, dout, (size_t)n_ * n, s));
         if (wait(s, err)) return -1;
         memcpy(out, hout, bytes);
         return 0;
@@ -182,9 +197,9 @@ class RcclComm : public Comm {
         if (cstream_) s = cstream_;
         if (stage(n * 8, s, err)) return -1;
         memcpy(hstage_, v, n * 8);
-        COMM_HIP(hipMemcpyAsync(stage_, hstage_, n * 8, hipMemcpyHostToDevice, s));
+        COMM_HIP(comm_copy(static_cast<uint64_t *>(stage_), static_cast<const uint64_t *>(hstage_dev_), n, s));
         if (nccl(api_->AllReduce(stage_, stage_, n, ncclUint64, ncclSum, cm, s), err)) return -1;
-        COMM_HIP(hipMemcpyAsync(hstage_, stage_, n * 8, hipMemcpyDeviceToHost, s));
+        COMM_HIP(comm_copy(static_cast<uint64_t *>(hstage_dev_), static_cast<const uint64_t *>(stage_), n, s));
         if (wait(s, err)) return -1;
         memcpy(v, hstage_, n * 8);
         return 0;
@@ -291,18 +306,19 @@ class RcclComm : public Comm {
             if (el > 0.002) usleep(50);
         }
     }
-    // the device and pinned host staging buffers of the small collectives (pageable host memory would
-    // make hipMemcpyAsync wait for the stream on the host, outside the bounded wait); the stream that
+    // the device and mapped pinned host staging buffers of the small collectives (a pageable or small
+    // hipMemcpyAsync can wait for the stream on the host, outside the bounded wait); the stream that
     // last used them has drained (every collective ends in a wait on it), so they can be replaced
     int stage(size_t bytes, hipStream_t s, std::string &err) {
         (void)s;
         if (stage_bytes_ >= bytes) return 0;
         if (stage_) (void)hipFree(stage_);
         if (hstage_) (void)hipHostFree(hstage_);
-        stage_ = hstage_ = nullptr;
+        stage_ = hstage_ = hstage_dev_ = nullptr;
         stage_bytes_ = 0;
         COMM_HIP(hipMalloc(&stage_, bytes));
-        COMM_HIP(hipHostMalloc(&hstage_, bytes, hipHostMallocDefault));
+        COMM_HIP(hipHostMalloc(&hstage_, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+        COMM_HIP(hipHostGetDevicePointer(&hstage_dev_, hstage_, 0));
         stage_bytes_ = bytes;
         return 0;
     }
@@ -310,7 +326,7 @@ class RcclComm : public Comm {
     ncclComm_t comm_;
     ncclComm_t ccomm_ = nullptr;    // the counts' communicator (split off comm_)
     hipStream_t cstream_ = nullptr; // ... and its stream
-    void *stage_ = nullptr, *hstage_ = nullptr;
+    void *stage_ = nullptr, *hstage_ = nullptr, *hstage_dev_ = nullptr;
     size_t stage_bytes_ = 0;
     double timeout_s_;
     bool aborted_ = false;

@@ -643,20 +643,22 @@ def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged):
     assert_same_as_oracle(kc, ref)
 
 
-@pytest.mark.parametrize("bits,use_ht", [(6, False), (16, False), (16, True)])
-def test_w128_fingerprint_collisions_counted_exactly(bits, use_ht):
-    # the 128-bit wave tier dedupes on 64-bit fingerprints and checks every key against its slot's
-    # claimer; with the fingerprints cut to `bits` bits (fk_debug_fingerprint_bits) distinct keys
-    # share them -- on every bucket at 6 bits, on about half at 16 -- and those buckets take the exact
-    # count from registers; the result stays bit-exact (repeated reads: multi-copy keys included)
+@pytest.mark.parametrize("k,m,bits,use_ht", [(55, 12, 6, False), (55, 12, 16, False), (55, 12, 16, True),
+                                              (28, 10, 6, False), (28, 10, 14, False), (28, 10, 14, True)])
+def test_wave_fingerprint_collisions_counted_exactly(k, m, bits, use_ht):
+    # the fingerprint wave tiers (128-bit keys: 64-bit fingerprints; 64-bit keys with FK_W64_FP: 32-bit
+    # fingerprints of the offset in the bucket) check every key against its slot's claimer; with the
+    # fingerprints cut to `bits` bits (fk_debug_fingerprint_bits) distinct keys share them -- on every
+    # bucket at 6 bits, on many at 14 / 16 -- and those buckets take the exact count from LDS; the
+    # result stays bit-exact (repeated reads: multi-copy keys included)
     rep = b"".join(b">q%d\n" % i + b"ACGTTGCAAGGCTTACCGATCGGATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAG"
                    b"CATGCATGCATCGACGTAGCATCG\n" for i in range(500))
     fasta = fk.synth_fasta(20_000, 150, 2_000_000, seed=0xF9 + bits) + rep
     L = fk.lib()
     assert L.fk_debug_fingerprint_bits(0, bits) == 0
     try:
-        kc = run_counter(fasta, 55, 12, 3, 64, use_ht)
-        ref = oracle.OracleResult(fasta, 55, 12, 64, threads=4)
+        kc = run_counter(fasta, k, m, 3, 64, use_ht)
+        ref = oracle.OracleResult(fasta, k, m, 64, threads=4)
         assert kc.stats()["kmers"] == ref.total_kmers
         assert_same_as_oracle(kc, ref, ordered=not use_ht)
     finally:
