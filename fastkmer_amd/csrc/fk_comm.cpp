@@ -10,6 +10,7 @@
 #include <sched.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -150,6 +151,7 @@ class RcclComm : public Comm {
         if (cstream_) (void)hipStreamSynchronize(cstream_);
         if (stage_) (void)hipFree(stage_);
         if (hstage_) (void)hipHostFree(hstage_);
+        for (auto &r : retired_) (void)hipFree(r.first), (void)hipHostFree(r.second);
         if (cstream_) (void)hipStreamDestroy(cstream_);
         if (ccomm_) (void)api_->CommDestroy(ccomm_);
         if (comm_) (void)api_->CommDestroy(comm_);
@@ -309,11 +311,13 @@ class RcclComm : public Comm {
     // the device and mapped pinned host staging buffers of the small collectives (a pageable or small
     // hipMemcpyAsync can wait for the stream on the host, outside the bounded wait); the stream that
     // last used them has drained (every collective ends in a wait on it), so they can be replaced
+    //    A grown buffer's predecessors are kept until the communicator is destroyed: hipFree
+    //    synchronizes the device, which blocks for good behind a collective that never completes.
     int stage(size_t bytes, hipStream_t s, std::string &err) {
         (void)s;
         if (stage_bytes_ >= bytes) return 0;
-        if (stage_) (void)hipFree(stage_);
-        if (hstage_) (void)hipHostFree(hstage_);
+        bytes = std::max<size_t>(bytes, std::max<size_t>(2 * stage_bytes_, 1u << 20));
+        if (stage_) retired_.push_back({stage_, hstage_});
         stage_ = hstage_ = hstage_dev_ = nullptr;
         stage_bytes_ = 0;
         COMM_HIP(hipMalloc(&stage_, bytes));
@@ -327,6 +331,7 @@ class RcclComm : public Comm {
     ncclComm_t ccomm_ = nullptr;    // the counts' communicator (split off comm_)
     hipStream_t cstream_ = nullptr; // ... and its stream
     void *stage_ = nullptr, *hstage_ = nullptr, *hstage_dev_ = nullptr;
+    std::vector<std::pair<void *, void *>> retired_;  // (device, host) staging buffers outgrown
     size_t stage_bytes_ = 0;
     double timeout_s_;
     bool aborted_ = false;

@@ -317,7 +317,7 @@ int fk_debug_comm_held(fk_ctx *ctx);
 
 /* Test hook: the 128-bit wave tier (33 <= k <= 63) dedupes on 64-bit key
  * fingerprints and checks every key against its slot's claimer; a shared
- * fingerprint sends the bucket to an exact count from registers.  This cuts
+ * fingerprint sends the bucket to an exact count from LDS.  This cuts
  * the fingerprints of `device` to their low `bits` bits (0: whole, the
  * product), so that tests drive that path on every bucket. */
 int fk_debug_fingerprint_bits(int32_t device, int32_t bits);

@@ -644,13 +644,12 @@ def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged):
 
 
 @pytest.mark.parametrize("k,m,bits,use_ht", [(55, 12, 6, False), (55, 12, 16, False), (55, 12, 16, True),
-                                              (28, 10, 6, False), (28, 10, 14, False), (28, 10, 14, True)])
+                                              (40, 9, 10, False)])
 def test_wave_fingerprint_collisions_counted_exactly(k, m, bits, use_ht):
-    # the fingerprint wave tiers (128-bit keys: 64-bit fingerprints; 64-bit keys with FK_W64_FP: 32-bit
-    # fingerprints of the offset in the bucket) check every key against its slot's claimer; with the
-    # fingerprints cut to `bits` bits (fk_debug_fingerprint_bits) distinct keys share them -- on every
-    # bucket at 6 bits, on many at 14 / 16 -- and those buckets take the exact count from LDS; the
-    # result stays bit-exact (repeated reads: multi-copy keys included)
+    # the 128-bit wave tier dedupes on 64-bit fingerprints and checks every key against its slot's
+    # claimer; with the fingerprints cut to `bits` bits (fk_debug_fingerprint_bits) distinct keys share
+    # them -- on every bucket at 6 bits, on many at 10 / 16 -- and those buckets take the exact count from
+    # LDS; the result stays bit-exact (repeated reads: multi-copy keys included)
     rep = b"".join(b">q%d\n" % i + b"ACGTTGCAAGGCTTACCGATCGGATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAG"
                    b"CATGCATGCATCGACGTAGCATCG\n" for i in range(500))
     fasta = fk.synth_fasta(20_000, 150, 2_000_000, seed=0xF9 + bits) + rep
