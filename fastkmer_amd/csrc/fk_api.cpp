@@ -284,6 +284,10 @@ struct fk_ctx {
     void *pinned[2] = {nullptr, nullptr};  // staging for pageable sources
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr;     // H2D of fk_ingest (the map runs on `stream` meanwhile)
+    hipStream_t tier_side = nullptr;       // the count's heavy tiers beside the wave tier (FK_TIER_SIDE)
+    // [0] cut -> wave tier, [1] heavy tiers -> result, [2] last piece's cell offsets -> cut, [3] -> heavy
+    hipEvent_t side_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool cut_side = false;                 // the last staged piece: the job's bucket cut beside its expansion
     hipEvent_t seg_ev = nullptr;           // "segment landed" (copy stream -> map stream)
     hipEvent_t h2d_ev[2] = {nullptr, nullptr};  // first copy issued / last copy done (timing)
     // streamed map (fused path): fk_ingest maps every tile whose bytes (and halo) have landed
@@ -602,6 +606,8 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     // later segments never queues behind a piece's expansion; the exchange: the received segments)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xstage, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xstage_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->tier_side, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->side_ev[i], hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreate(&c->h2d_ev[i]);
     if (e != hipSuccess) {
         fk_destroy(c);
@@ -691,6 +697,9 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
     release(c->piece_starts);
     if (c->seg_ev) (void)hipEventDestroy(c->seg_ev);
     for (auto &ev : c->h2d_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->tier_side) (void)hipStreamSynchronize(c->tier_side), (void)hipStreamDestroy(c->tier_side);
+    for (auto &ev : c->side_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -1615,6 +1624,7 @@ static int sorted_expand(fk_ctx *c, const SortedPlan &pl, uint32_t nchunks, uint
                                    c->cell_total.as<uint64_t>(), s));
     }
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), cell_base, ncell_all, cell_base + ncell_all, c->ws, s));
+    if (c->cut_side) HIP_TRY(hipEventRecord(c->side_ev[2], s));  // the cell totals and offsets are ready
     if (two_level) {
         FK_TRY(ensure(c->mid, total_kmers * 8 * c->KW));
         HIP_TRY(launch_expand_two_level(c->KW, c->rsrc, c->chunks.as<Chunk>(), nchunks, c->nlb, k, F,
@@ -1660,6 +1670,8 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                                 const uint64_t *cell_total, const uint64_t *cell_base, CountBufs B, DevBuf &okb,
                                 uint64_t *nb_out) {
     hipStream_t s = c->stream;
+    // the cut's stream: `s`, or beside the last staged piece's expansion (cut_side)
+    const hipStream_t cs = c->cut_side ? c->tier_side : s;
     const int k = c->cfg.k;
     const int F = pl.F;
     const bool tiered = pl.tiered;
@@ -1676,31 +1688,31 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
     // <= wave_cap keys for the wave kernel, larger cells to the block kernel
     // (<= cap) or the large path.  Otherwise buckets of <= cap keys.
     if (tiered)
-        HIP_TRY(launch_bucket_flags_greedy(cell_total, c->nlb, F, wave_cap, -1, B.flags->as<uint32_t>(), s));
+        HIP_TRY(launch_bucket_flags_greedy(cell_total, c->nlb, F, wave_cap, -1, B.flags->as<uint32_t>(), cs));
     else
-        HIP_TRY(launch_bucket_flags(cell_base, cell_total, c->nlb, F, cap / 4, cap - cap / 4, B.flags->as<uint32_t>(), s));
+        HIP_TRY(launch_bucket_flags(cell_base, cell_total, c->nlb, F, cap / 4, cap - cap / 4, B.flags->as<uint32_t>(), cs));
     HIP_TRY(scan_excl_sum_u32_to_u64(B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), ncell_all,
-                                     B.flag_scan->as<uint64_t>() + ncell_all, c->ws, s));
+                                     B.flag_scan->as<uint64_t>() + ncell_all, c->ws, cs));
     uint64_t nbuckets = 0;
-    HIP_TRY(hipMemcpyAsync(&nbuckets, B.flag_scan->as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpyAsync(&nbuckets, B.flag_scan->as<uint64_t>() + ncell_all, 8, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
     htrace("sorted: nbuckets read");
     FK_TRY(ensure(*B.buckets, nbuckets * sizeof(Bucket)));
     FK_TRY(ensure(okb, total_kmers * 8 * c->KW));
     FK_TRY(ensure(*B.out_counts, total_kmers * 4));
     FK_TRY(ensure(*B.bucket_unique, (nbuckets + 1) * 8));
     HIP_TRY(launch_bucket_write(cell_base, B.flags->as<uint32_t>(), B.flag_scan->as<uint64_t>(), c->nlb, F, nbuckets,
-                                total_kmers, B.buckets->as<Bucket>(), s));
+                                total_kmers, B.buckets->as<Bucket>(), cs));
     BucketSrc src = src_in;
     src.F = F;
     if (src.np > 0) FK_TRY(ensure(*B.piece_starts, nbuckets * sizeof(PieceStarts)));
     // the buckets' sizes, and the staged pieces' starts per bucket (read by the wave tier)
     HIP_TRY(launch_bucket_finish(src, B.buckets->as<Bucket>(), nbuckets, c->nlb, total_kmers,
-                                 src.np > 0 ? B.piece_starts->as<PieceStarts>() : nullptr, s));
+                                 src.np > 0 ? B.piece_starts->as<PieceStarts>() : nullptr, cs));
     if (src.np > 0) src.starts = B.piece_starts->as<PieceStarts>();
     // 5: exact count per bucket in LDS; buckets that do not fit take the streaming path
     const uint32_t small_limit = c->force_large ? 0u : cap;
-    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, cs));
     c->stats.buckets = nbuckets;
     c->stats.fine_bits = (uint64_t)F;
     c->stats.heavy_keys = 0;
@@ -1717,13 +1729,28 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
         const uint32_t block_top = FK_SPLIT_HEAVY ? (c->KW == 1 ? WAVE_MID_CAP : WAVE128_MID_CAP) : cap;
         HIP_TRY(launch_bucket_tiers(B.buckets->as<Bucket>(), nbuckets, wave_cap, block_top,
                                     B.bucket_unique->as<uint64_t>(), lists, c->misc.as<unsigned int>(),
-                                    c->misc.as<unsigned long long>() + 3, s));
+                                    c->misc.as<unsigned long long>() + 3, cs));
         // the tier sizes (and the listed buckets' keys) go to pinned memory right behind the tier
         // kernel: the host waits for that copy, not for the wave tier queued after it, before it
         // queues the heavier tiers
         if (c->pin_tier.ensure(64)) return set_err(FK_E_NOMEM, "hipHostMalloc failed");
-        HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 32, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipEventRecord(c->tier_ev, s));
+        HIP_TRY(hipMemcpyAsync(c->pin_tier.p, c->misc.p, 32, hipMemcpyDeviceToHost, cs));
+        HIP_TRY(hipEventRecord(c->tier_ev, cs));
+#ifndef FK_TIER_SIDE
+#define FK_TIER_SIDE 1  // A/B builds: -DFK_TIER_SIDE=0 the heavy tiers queued behind the wave tier
+#endif
+        // the heavier tiers (split, in-order sub-buckets, mid wave tier, fallbacks) run on their own
+        // stream beside the wave tier: their buckets, outputs and counters are disjoint from its, and
+        // the host's waits for the split's counts no longer wait for the wave tier
+        const hipStream_t hs = (FK_TIER_SIDE && c->tier_side) ? c->tier_side : s;
+        if (cs != s) {  // the wave tier after the cut (and, in stream order, the last piece's expansion)
+            HIP_TRY(hipEventRecord(c->side_ev[0], cs));
+            HIP_TRY(hipStreamWaitEvent(s, c->side_ev[0], 0));
+        }
+        if (hs != s) {  // the heavy tiers after both as well
+            HIP_TRY(hipEventRecord(c->side_ev[3], s));
+            HIP_TRY(hipStreamWaitEvent(hs, c->side_ev[3], 0));
+        }
         // every bucket of <= wave_cap keys
         if (c->KW == 1)
             HIP_TRY(launch_bucket_count64_wave(src, B.buckets->as<Bucket>(), nbuckets, k,
@@ -1765,20 +1792,20 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
                 uint32_t *fb = c->sp_fb.as<uint32_t>();
                 unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
-                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(), s));
+                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(), hs));
                 HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
-                                          c->sp_base.as<uint64_t>() + nl, c->ws, s));
+                                          c->sp_base.as<uint64_t>() + nl, c->ws, hs));
                 if (w1)
                     HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, 0, l1, nl,
                                                   c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
                                                   c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb,
-                                                  fb + nl, cap, k, F, s));
+                                                  fb + nl, cap, k, F, hs));
                 else
                     HIP_TRY(launch_bucket_split128(src, B.buckets->as<Bucket>(), l1, nl, c->sp_base.as<uint64_t>(),
                                                    c->sp_keys.as<uint64_t>(), c->sp_subs.as<SubBucket128>(),
-                                                   c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, s));
-                HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipEventRecord(c->tier_ev, s));
+                                                   c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, hs));
+                HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, hs));
+                HIP_TRY(hipEventRecord(c->tier_ev, hs));
                 HIP_TRY(hipEventSynchronize(c->tier_ev));
                 const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
                 const uint32_t nsub = sc[0];
@@ -1823,12 +1850,12 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     HIP_TRY(launch_sub_count64_seq(B.buckets->as<Bucket>(), l1, nl, c->sp_par.as<SplitParent>(),
                                                    c->sp_subs.as<SubBucket>(), c->sp_keys.as<uint64_t>(),
                                                    okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                   B.bucket_unique->as<uint64_t>(), s, ordered));
+                                                   B.bucket_unique->as<uint64_t>(), hs, ordered));
                 else
                     HIP_TRY(launch_sub_count128_seq(B.buckets->as<Bucket>(), l1, nl, c->sp_par.as<SplitParent>(),
                                                     c->sp_subs.as<SubBucket128>(), c->sp_keys.as<uint64_t>(),
                                                     okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                    B.bucket_unique->as<uint64_t>(), s, ordered));
+                                                    B.bucket_unique->as<uint64_t>(), hs, ordered));
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
@@ -1837,33 +1864,37 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 if (w1)
                     HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                            okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                           B.bucket_unique->as<uint64_t>(), s, ordered));
+                                                           B.bucket_unique->as<uint64_t>(), hs, ordered));
                 else
                     HIP_TRY(launch_bucket_count128_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                             okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                            B.bucket_unique->as<uint64_t>(), s, ordered));
+                                                            B.bucket_unique->as<uint64_t>(), hs, ordered));
                 if (block_top > mid_cap)  // no split: the block tier's buckets above the mid wave tier
-                    FK_TRY(block_tier(c, src, B, okb, lists, ntier[0], cap, mid_cap, s));
+                    FK_TRY(block_tier(c, src, B, okb, lists, ntier[0], cap, mid_cap, hs));
             }
-            if (nfbB) FK_TRY(block_tier(c, src, B, okb, fbB, nfbB, cap, 0, s));
+            if (nfbB) FK_TRY(block_tier(c, src, B, okb, fbB, nfbB, cap, 0, hs));
             if (nfbG && w1) {
                 // above 2048 keys with at most 4096 distinct in one workgroup's LDS; others stay REDO
                 HIP_TRY(launch_bucket_count64_big(src, B.buckets->as<Bucket>(), nfbG, k, okb.as<uint64_t>(),
                                                   B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                  c->misc.as<unsigned long long>() + 2, fbG, s));
-                HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
+                                                  c->misc.as<unsigned long long>() + 2, fbG, hs));
+                HIP_TRY(hipMemcpyAsync(&nlarge, c->misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, hs));
+                HIP_TRY(hipStreamSynchronize(hs));
             } else if (nfbG) {
                 nlarge = nfbG;  // 128-bit keys: no big-table kernel
             }
             if (nlarge) {  // scratch for the listed buckets' keys only, taken by a cursor
                 FK_TRY(ensure(c->scratch, listed_keys * 8 * c->KW));
-                HIP_TRY(hipMemsetAsync(c->misc.as<unsigned long long>() + 6, 0, 8, s));
+                HIP_TRY(hipMemsetAsync(c->misc.as<unsigned long long>() + 6, 0, 8, hs));
                 HIP_TRY(launch_bucket_sort_large(c->KW, src, B.buckets->as<Bucket>(), nfbG, k,
                                                  c->scratch.as<uint64_t>(), okb.as<uint64_t>(),
                                                  B.out_counts->as<uint32_t>(), B.bucket_unique->as<uint64_t>(),
-                                                 fbG, s, c->misc.as<unsigned long long>() + 6));
+                                                 fbG, hs, c->misc.as<unsigned long long>() + 6));
             }
+        }
+        if (hs != s) {  // the result's scans follow both streams
+            HIP_TRY(hipEventRecord(c->side_ev[1], hs));
+            HIP_TRY(hipStreamWaitEvent(s, c->side_ev[1], 0));
         }
         c->stats.oversize_buckets = nlarge;
     } else {
@@ -2231,7 +2262,13 @@ static int staged_expand_chunks(fk_ctx *c, uint32_t nchunks, const std::vector<u
     FK_TRY(sorted_expand(c, pl, nchunks, pk, c->st_keys[p], c->st_cb[p]));
     const uint64_t ncell_all = (uint64_t)c->nlb << c->st_plan.F;
     FK_TRY(ensure(c->st_total, ncell_all * 8));
-    HIP_TRY(launch_add_u64(c->st_total.as<uint64_t>(), c->cell_total.as<uint64_t>(), ncell_all, p == 0, s));
+    if (c->cut_side) {  // the job's cell totals on the cut's stream, while this piece is expanded
+        HIP_TRY(hipStreamWaitEvent(c->tier_side, c->side_ev[2], 0));
+        HIP_TRY(launch_add_u64(c->st_total.as<uint64_t>(), c->cell_total.as<uint64_t>(), ncell_all, p == 0,
+                               c->tier_side));
+    } else {
+        HIP_TRY(launch_add_u64(c->st_total.as<uint64_t>(), c->cell_total.as<uint64_t>(), ncell_all, p == 0, s));
+    }
     HIP_TRY(hipEventRecord(c->st_ev[4 * p + 3], s));
     c->st_kmers += pk;
     c->st_np = p + 1;
@@ -2262,8 +2299,12 @@ static int staged_count(fk_ctx *c) {
     HIP_TRY(hipEventRecord(c->ev[6], s));
     std::swap(c->cell_total, c->st_total);  // the job's cell totals (st_total is rebuilt by the next job)
     FK_TRY(ensure(c->cell_base, (ncell_all + 1) * 8));
+    // the bucket cut (this scan, sorted_count_buckets' flags, buckets and tiers) on the cut's stream when
+    // the last piece is still being expanded on `s` (cut_side)
+    const hipStream_t cs = c->cut_side ? c->tier_side : s;
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(cs, c->side_ev[2], 0));
     HIP_TRY(scan_excl_sum_u64(c->cell_total.as<uint64_t>(), c->cell_base.as<uint64_t>(), ncell_all,
-                              c->cell_base.as<uint64_t>() + ncell_all, c->ws, s));
+                              c->cell_base.as<uint64_t>() + ncell_all, c->ws, cs));
     BucketSrc src{nullptr, pl.F};
     src.np = (int)c->st_np;
     for (uint32_t p = 0; p < c->st_np; ++p) {
@@ -2738,12 +2779,25 @@ static int finish_local(fk_ctx *c) {
     DeviceGuard dg_(c->device);
     if (c->st_np && c->rec_tiled && !c->pieces_void && c->tiles_counted <= c->rec_tiles) {
         // staged pieces were expanded while the input landed: the last piece, then one count
+#ifndef FK_CUT_SIDE
+#define FK_CUT_SIDE 1  // A/B builds: -DFK_CUT_SIDE=0 the bucket cut after the last piece's expansion
+#endif
+        // the job's bucket cut needs the last piece's cell totals, not its keys: it runs on the side
+        // stream while the piece's two expansion levels run on `stream`
+        int rc = FK_OK;
+        c->cut_side = FK_CUT_SIDE && c->tier_side && c->rec_tiles > c->tiles_counted;
+        // the cut's stream starts after everything queued so far (re-recorded once the last piece's cell
+        // offsets are scanned; a piece without k-mers records nothing more)
+        if (c->cut_side) HIP_TRY(hipEventRecord(c->side_ev[2], c->stream));
         if (c->rec_tiles > c->tiles_counted) {
             const uint64_t t0 = c->tiles_counted, nt = c->rec_tiles - t0;
-            FK_TRY(staged_expand(c, fused_src(c, t0, nt, nt * map_fused_tcap()),
-                                 c->job_bytes ? (double)(nt * fm_tile_bytes(FUSED_NT)) / (double)c->job_bytes : 0.0));
+            rc = staged_expand(c, fused_src(c, t0, nt, nt * map_fused_tcap()),
+                               c->job_bytes ? (double)(nt * fm_tile_bytes(FUSED_NT)) / (double)c->job_bytes : 0.0);
         }
-        FK_TRY(staged_count(c));
+        if (rc == FK_OK) rc = staged_count(c);
+        if (c->cut_side) (void)hipStreamSynchronize(c->tier_side);
+        c->cut_side = false;
+        FK_TRY(rc);
         pieces_reset(c);
         return FK_OK;
     }
