@@ -1541,13 +1541,19 @@ static SortedPlan sorted_plan(const fk_ctx *c, uint64_t max_bin_kmers) {
     // cell bits: the largest bin's cells average cap/4 keys (a bucket groups a
     // few cells; runs of one chunk's keys per cell stay long enough to be
     // written as whole lines)
-    // (two-level expansion: cap / 8, measured faster; the wave tier then holds
-    // nearly every cell)
+    // (two-level expansion, 64-bit keys: 512 since round 6 -- half the cells of
+    // round 2's cap / 8, so the bucket cut and the last piece's level 2 touch
+    // half the cell words: configs[2] load 146.9 -> 146.3 ms, configs[1] equal,
+    // profiles/r06r_cell_target.txt; 128-bit keys keep 128 per cell)
     // k = 64 (no spare bit in a 128-bit key's hi word): one-level scatter, one workgroup per bucket
     const bool tiered = c->cfg.k <= 63 && c->dbg_phase == 99 && !c->force_large;
     const bool two_level = c->cfg.k <= 63;
+#ifndef FK_CELL_TARGET64
+#define FK_CELL_TARGET64 512  // A/B builds: keys per cell of the largest bin, 64-bit keys, two levels
+#endif
     const uint64_t target = c->cell_target ? c->cell_target
-                                           : (c->KW == 2 && tiered ? WAVE128_BUCKET_CAP / 2 : two_level ? cap / 8 : cap / 4);
+                                           : (c->KW == 2 && tiered ? WAVE128_BUCKET_CAP / 2
+                                                                   : two_level ? FK_CELL_TARGET64 : cap / 4);
     int F = 1;
     while (F < MAX_FINE_BITS && ((uint64_t)1 << F) * target < max_bin_kmers) ++F;
     if (!two_level) F = std::min(F, MAX_FINE_BITS - 1);  // one-level scatter: 8 << F bytes of LDS <= 128 KB

@@ -407,10 +407,12 @@ def test_full_size_properties():
 
 
 @pytest.mark.parametrize("k,m", [(28, 10), (55, 12)])
-def test_max_fine_bits_one_bin_vs_oracle(k, m):
-    # B = 1: every k-mer in one bin (4.4 M at k = 28, 2.8 M at k = 55), past 2^14 cells of the
-    # cell target, so the bin is cut into the most cells (F = MAX_FINE_BITS = 15: the histogram,
-    # flag and scatter kernels at 128 KB of LDS) -- the largest-F path against the oracle
+def test_max_fine_bits_one_bin_vs_oracle(monkeypatch, k, m):
+    # B = 1: every k-mer in one bin (4.4 M at k = 28, 2.8 M at k = 55), past 2^14 cells of 128 keys
+    # (FASTKMER_DEBUG_CELL_TARGET; 64-bit keys default to 512 per cell), so the bin is cut into the
+    # most cells (F = MAX_FINE_BITS = 15: the histogram, flag and scatter kernels at 128 KB of LDS) --
+    # the largest-F path against the oracle
+    monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", "128")
     fasta = fk.synth_fasta(60_000, 100, 10_000_000, seed=67)
     kc = run_counter(fasta, k, m, 3, 1)
     st = kc.stats()
