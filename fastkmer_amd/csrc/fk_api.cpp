@@ -263,6 +263,7 @@ struct fk_ctx {
     // Test hooks (result-preserving; they steer inputs that FASTA data cannot aim at onto a path):
     bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS=1: route every bucket through the streaming path
     uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: auto)
+    int mid_parts = -1;        // FASTKMER_DEBUG_MID_PARTS: the mid tier's key ranges always (1) / never (0) / by size (-1)
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
     // Measurement-only (a library built with -DFK_PROBES; wrong results by design):
@@ -323,6 +324,7 @@ struct fk_ctx {
     DevBuf scratch;
     DevBuf bucket_unique, dense_off, dense_keys, dense_counts, bin_off, misc, tier_list, mid, sc_total;
     DevBuf sp_base, sp_keys, sp_subs, sp_par, sp_fb;  // heavy buckets split into sub-buckets
+    DevBuf mid_fb;  // mid-tier buckets left to the 1024-key kernel by the ranges kernel
     ScanWorkspace ws;
     // results
     bool have_result = false;
@@ -569,6 +571,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *v = env("FASTKMER_INGEST_SEG")) c->ingest_seg = std::max(1ull << 16, strtoull(v, nullptr, 10));
     if (const char *v = env("FASTKMER_DEBUG_LARGE_BUCKETS")) c->force_large = v[0] == '1';
     if (const char *v = env("FASTKMER_DEBUG_CELL_TARGET")) c->cell_target = (uint32_t)atoi(v);
+    if (const char *v = env("FASTKMER_DEBUG_MID_PARTS")) c->mid_parts = atoi(v);  // test hook: 1 always, 0 never
     if (const char *v = env("FASTKMER_X2_L1")) c->x2_l1 = atoi(v);
     if (const char *v = env("FASTKMER_FUSED")) c->fused = atoi(v);
 #ifdef FK_PROBES
@@ -652,7 +655,7 @@ FK_EXPORT void fk_destroy(fk_ctx *c) {
                       &c->cell_total, &c->cell_base, &c->flags, &c->flag_scan, &c->buckets, &c->keys,
                       &c->out_keys, &c->out_counts, &c->bucket_unique, &c->dense_off, &c->dense_keys,
                       &c->dense_counts, &c->bin_off, &c->misc, &c->tier_list, &c->mid, &c->sc_total, &c->gather_keys, &c->gather_counts,
-                      &c->sp_base, &c->sp_keys, &c->sp_subs, &c->sp_par, &c->sp_fb};
+                      &c->sp_base, &c->sp_keys, &c->sp_subs, &c->sp_par, &c->sp_fb, &c->mid_fb};
     for (DevBuf *b : bufs) release(*b);
     for (int i = 0; i < 2; ++i) {
         if (c->pinned[i]) (void)hipHostFree(c->pinned[i]);
@@ -1787,6 +1790,25 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             const uint32_t *l1 = lists + nbuckets;
             uint32_t *fbB = nullptr, *fbG = lists + nbuckets;  // the fallback lists (block / big)
             uint32_t nfbB = 0, nfbG = ntier[1];
+#ifndef FK_MID_PARTS
+#define FK_MID_PARTS 1  // A/B builds: -DFK_MID_PARTS=0 the 64-bit mid tier's buckets all on the 1024-key kernel
+#endif
+            constexpr uint32_t MID_PARTS_MIN = 1u << 17;  // mid-tier buckets from which the ranges kernel pays
+            // 64-bit mid tier: 2 or 3 key ranges per bucket on the wave tier's table (k_bucket_count64_parts);
+            // the buckets it leaves (a range above 512 keys) are listed for the 1024-key kernel.  Only for a
+            // large mid tier: the configs[2] load's 278 K mid buckets 146.5 -> 146.2 ms, but configs[1]'s 59 K
+            // 21.8 -> 21.95 ms (profiles/r06v_mid_parts_ab.txt)
+            const bool parts = FK_MID_PARTS && w1 && ntier[0] && block_top == WAVE_MID_CAP && c->mid_parts != 0 &&
+                               (c->mid_parts == 1 || ntier[0] >= MID_PARTS_MIN);
+            uint32_t *mid_fb = nullptr, nmidfb = 0;
+            unsigned int *mid_fbc = c->misc.as<unsigned int>() + 11;
+            if (parts) {
+                FK_TRY(ensure(c->mid_fb, (uint64_t)ntier[0] * 4));
+                mid_fb = c->mid_fb.as<uint32_t>();
+                HIP_TRY(launch_bucket_count64_parts(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                    okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                    B.bucket_unique->as<uint64_t>(), mid_fb, mid_fbc, hs, ordered));
+            }
             if (FK_SPLIT_HEAVY && ntier[1]) {  // nothing to split: no split kernels, no read-back
                 const uint32_t nl = ntier[1];
                 const uint64_t maxsub = listed_keys / 64 + nl + 64;  // >= ceil(n / SPL_TGT) sub-buckets per bucket
@@ -1810,11 +1832,12 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     HIP_TRY(launch_bucket_split128(src, B.buckets->as<Bucket>(), l1, nl, c->sp_base.as<uint64_t>(),
                                                    c->sp_keys.as<uint64_t>(), c->sp_subs.as<SubBucket128>(),
                                                    c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, hs));
-                HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 12, hipMemcpyDeviceToHost, hs));
+                HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 16, hipMemcpyDeviceToHost, hs));
                 HIP_TRY(hipEventRecord(c->tier_ev, hs));
                 HIP_TRY(hipEventSynchronize(c->tier_ev));
                 const uint32_t *sc = c->pin_tier.as<uint32_t>() + 8;
                 const uint32_t nsub = sc[0];
+                nmidfb = sc[3];  // misc word 11: the ranges kernel's fallbacks (queued before the copy)
                 fbB = fb, nfbB = sc[1], fbG = fb + nl, nfbG = sc[2];
                 htrace("sorted: split counts read");
 #ifdef FK_PROBES
@@ -1865,9 +1888,20 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
+            if (parts && !(FK_SPLIT_HEAVY && ntier[1])) {  // no split read-back: the fallbacks' count alone
+                HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 44, mid_fbc, 4, hipMemcpyDeviceToHost, hs));
+                HIP_TRY(hipEventRecord(c->tier_ev, hs));
+                HIP_TRY(hipEventSynchronize(c->tier_ev));
+                nmidfb = c->pin_tier.as<uint32_t>()[11];
+            }
             const uint32_t mid_cap = w1 ? WAVE_MID_CAP : WAVE128_MID_CAP;
             if (ntier[0]) {
-                if (w1)
+                if (parts) {
+                    if (nmidfb)
+                        HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), mid_fb, nmidfb, k,
+                                                               okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                               B.bucket_unique->as<uint64_t>(), hs, ordered));
+                } else if (w1)
                     HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
                                                            okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
                                                            B.bucket_unique->as<uint64_t>(), hs, ordered));

@@ -237,6 +237,12 @@ hipError_t launch_bucket_tiers(const Bucket *buckets, uint64_t nb, uint32_t wave
 hipError_t launch_bucket_count64_wave(const BucketSrc &src, const Bucket *buckets, uint64_t nbuckets, int k,
                                       uint64_t *out_keys, uint32_t *out_counts, uint64_t *bucket_unique,
                                       const uint32_t *list, hipStream_t s, bool ordered = true);
+// the listed mid-tier buckets (WAVE_BUCKET_CAP .. WAVE_MID_CAP keys) as 2 or 3 key ranges, each counted
+// by the wave tier's code in order; buckets with a range above WAVE_BUCKET_CAP go to fb (count in fb_count)
+hipError_t launch_bucket_count64_parts(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
+                                       uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
+                                       uint64_t *bucket_unique, uint32_t *fb, unsigned int *fb_count, hipStream_t s,
+                                       bool ordered);
 // the listed block-tier buckets of at most WAVE_MID_CAP keys, one wave each (k <= 32)
 hipError_t launch_bucket_count64_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
                                           uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,

@@ -449,6 +449,35 @@ def test_block_and_big_tiers_vs_oracle(monkeypatch):
     assert_same_as_oracle(kc, ref)
 
 
+@pytest.mark.parametrize("cell_target,staged,use_ht", [(700, False, False), (700, True, False), (700, False, True),
+                                                      (400, False, False)])
+def test_mid_tier_key_ranges_vs_oracle(monkeypatch, cell_target, staged, use_ht):
+    # cells of ~700 (~400) keys: many buckets of 513..1024 keys, which the 64-bit mid tier counts as 2 or 3
+    # key ranges on the wave tier's table (k_bucket_count64_parts); 600 copies of a few reads put k-mers
+    # repeated 600 times into some of them, a range above 512 keys that the 1024-key kernel takes over
+    monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", str(cell_target))
+    monkeypatch.setenv("FASTKMER_DEBUG_MID_PARTS", "1")  # the product takes the ranges kernel from 2^17 mid buckets
+    rep = b"".join(b">r%d\n" % i + b"GATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAGCATGCATGCATCGACGTAGCATCG"
+                   b"ACGTTGCAAGGCTTACCGATCGG\n" for i in range(600))
+    fasta = fk.synth_fasta(200_000, 100, 3_000_000_000, seed=0x7A + cell_target) + rep
+    if staged:
+        import torch
+        monkeypatch.setenv("FASTKMER_INGEST_SEG", str(1 << 20))
+        monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(2 << 20))
+        host = torch.frombuffer(bytearray(fasta), dtype=torch.uint8).pin_memory()
+        kc = fk.KmerCounter(28, 10, 3, 16, use_ht=use_ht)
+        kc.ingest_ptr(host.data_ptr(), host.numel())
+        kc.finish()
+        assert kc.stats()["pieces_counted"] > 1
+    else:
+        kc = run_counter(fasta, 28, 10, 3, 16, use_ht=use_ht)
+    st = kc.stats()
+    assert st["block_buckets"] > (1000 if cell_target >= 700 else 100), st
+    ref = oracle.OracleResult(fasta, 28, 10, 16, threads=4)
+    assert st["kmers"] == ref.total_kmers
+    assert_same_as_oracle(kc, ref, ordered=not use_ht)
+
+
 @pytest.mark.parametrize("k,m", [(28, 10), (55, 12)])
 def test_wave_tables_of_distinct_keys_vs_oracle(k, m):
     # reads of a 3 Gbp virtual genome: nearly every k-mer is distinct, so the
