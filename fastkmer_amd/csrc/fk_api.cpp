@@ -370,6 +370,10 @@ struct fk_ctx {
     uint64_t reserve_bytes = 0;   // fk_ingest_reserve's size for the next job
     size_t segs_counted = 0;      // with a communicator: received segments [0, segs_counted) staged
     std::vector<double> st_cuts{0.4, 0.7, 0.9};  // piece ends of a staged job (FASTKMER_PIECE_CUTS; 45 / 70 / 85 % measured 22.84 vs 22.77 ms)
+    // ... of a 64-bit job of >= 4 GB without FASTKMER_PIECE_CUTS: five pieces, the last 7 % (configs[2]
+    // load 146.2 -> 145.4 ms, profiles/r06z_five_pieces.txt; configs[1]'s 1 GB keeps four)
+    std::vector<double> st_cuts5{0.38, 0.64, 0.82, 0.93};
+    bool cuts_env = false;
     // ... with a communicator: earlier, a received piece lands a step's partition and transfer later
     // (one in-process rank at the configs[2] load: 153.2-153.7 ms against 156.1-159.4 with the local
     // cuts, profiles/r05z_xch_cuts_seg_ab.txt)
@@ -565,6 +569,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
             const double f = strtod(q, &e);
             if (e == q) break;
             if (f > 0.0 && f < 1.0 && c->st_cuts.size() < STAGE_MAXP - 1) c->st_cuts.push_back(f), c->xst_cuts.push_back(f);
+            c->cuts_env = true;
             q = *e == ',' ? e + 1 : e;
         }
     }
@@ -2268,6 +2273,14 @@ static void pieces_reset(fk_ctx *c) {
     c->segs_counted = 0;
 }
 
+// Staged pieces per job: 128-bit keys at most STAGE_MAXP128 (their kernels' piece loops stop there)
+static uint32_t stage_maxp(const fk_ctx *c) { return c->KW == 2 ? (uint32_t)STAGE_MAXP128 : (uint32_t)STAGE_MAXP; }
+// one rank's piece ends: FASTKMER_PIECE_CUTS, five pieces for a 64-bit job of >= 4 GB, else four
+static const std::vector<double> &local_cuts(const fk_ctx *c) {
+    if (!c->cuts_env && c->KW == 1 && c->job_bytes >= (4ull << 30) && STAGE_MAXP >= 5) return c->st_cuts5;
+    return c->st_cuts;
+}
+
 // ---- staged pieces (sorted count, k <= 32): one rank's landed pieces, or the received segments
 // (k = 64 counts the whole input after the last byte; so do the test hook that routes every bucket
 // through the streaming path and the bucket-kernel probes)
@@ -2319,7 +2332,7 @@ static int staged_expand_chunks(fk_ctx *c, uint32_t nchunks, const std::vector<u
 // One rank: partitions a piece of the mapped tiles by local bin, then expands it.
 static int staged_expand(fk_ctx *c, const RecSrc &src, double frac) {
     const uint32_t p = c->st_np;
-    if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
+    if (p >= stage_maxp(c)) return set_err(FK_E_STATE, "more than %u staged pieces", stage_maxp(c));
     uint64_t nrecv = 0;
     std::vector<Chunk> chunks;
     std::vector<uint32_t> bcb;
@@ -2380,17 +2393,20 @@ static int staged_count(fk_ctx *c) {
 // Piece ends: with the job's size known (one fk_ingest call, or fk_ingest_reserve) and no
 // FASTKMER_PIECE_BYTES, at the fractions st_cuts of it (the last piece -- expanded after the last byte
 // lands -- is the smallest); jobs under 2 * MIN_PIECE are counted whole.  A streamed job of unknown
-// size: every piece_bytes.  At most STAGE_MAXP - 1 pieces before fk_finish stages the last one.
+// size: every piece_bytes, at most three pieces before fk_finish stages the last one (with cuts: at
+// most stage_maxp - 1).
 static bool local_piece_due(const fk_ctx *c, uint64_t tiles) {
     constexpr uint64_t MIN_PIECE = 256ull << 20;
-    if (c->st_np >= (uint32_t)STAGE_MAXP - 1) return false;
+    if (c->st_np >= stage_maxp(c) - 1) return false;
     const uint64_t tile = fm_tile_bytes(FUSED_NT);
     if (c->job_bytes && !c->piece_bytes_set) {
-        if (c->job_bytes < 2 * MIN_PIECE || c->st_cut >= c->st_cuts.size()) return false;
-        const uint64_t end = (uint64_t)(c->st_cuts[c->st_cut] * (double)c->job_bytes);
+        const std::vector<double> &cuts = local_cuts(c);
+        if (c->job_bytes < 2 * MIN_PIECE || c->st_cut >= cuts.size()) return false;
+        const uint64_t end = (uint64_t)(cuts[c->st_cut] * (double)c->job_bytes);
         return tiles * tile >= end && (tiles - c->tiles_counted) * tile >= MIN_PIECE / 2;
     }
-    return (tiles - c->tiles_counted) * tile >= c->piece_bytes;
+    // every piece_bytes: at most four pieces (three before fk_finish), as the exchange's
+    return c->st_np < 3 && (tiles - c->tiles_counted) * tile >= c->piece_bytes;
 }
 
 // The context's stream and scan workspace swapped for the staging stream's while a staging step is
@@ -2660,7 +2676,7 @@ static int segment_ranges(fk_ctx *c, size_t s0, size_t s1, std::vector<std::vect
 static int xch_stage_segments(fk_ctx *c, size_t s1, double frac) {
     if (s1 <= c->segs_counted) return FK_OK;
     const uint32_t p = c->st_np;
-    if (p >= (uint32_t)STAGE_MAXP) return set_err(FK_E_STATE, "more than %d staged pieces", STAGE_MAXP);
+    if (p >= stage_maxp(c)) return set_err(FK_E_STATE, "more than %u staged pieces", stage_maxp(c));
     StageStream ss_(c);
     hipStream_t s = c->stream;  // the staging stream
     // its earlier work (behind earlier steps' transfers) is done: bounded with a communicator
@@ -2694,7 +2710,8 @@ static double xch_recv_frac(const fk_ctx *c, uint64_t recs) {
 // Staged: the segments received before this step are expanded once they hold about 1 / STAGE_MAXP
 // of the job (every step when its size is unknown), at most STAGE_MAXP - 1 times before fk_finish.
 static int xch_maybe_stage(fk_ctx *c, size_t s1) {
-    if (c->st_np >= (uint32_t)STAGE_MAXP - 1 || s1 <= c->segs_counted) return FK_OK;
+    // (at most four pieces: the exchange's cuts are xst_cuts)
+    if (c->st_np >= std::min<uint32_t>(stage_maxp(c), 4) - 1 || s1 <= c->segs_counted) return FK_OK;
     uint64_t recs = 0, before = 0;
     for (size_t i = 0; i < s1; ++i)
         for (uint64_t n : c->xch.segs[i].rec) (i < c->segs_counted ? before : recs) += n;

@@ -45,10 +45,15 @@ struct Bucket {
 // counted once): piece p holds the bucket's keys at pk[p][pcb[p][g0] .. pcb[p][g1]), g0 / g1 =
 // (lbin << F) + c0 / c1, pcb[p] the exclusive scan of the piece's cell totals.
 #ifndef FK_STAGE_MAXP
-#define FK_STAGE_MAXP 4
+#define FK_STAGE_MAXP 5
 #endif
 constexpr int STAGE_MAXP = FK_STAGE_MAXP;
-static_assert(STAGE_MAXP >= 2 && STAGE_MAXP <= 8, "staged pieces per job");
+static_assert(STAGE_MAXP >= 4 && STAGE_MAXP <= 8, "staged pieces per job");
+// 128-bit keys (k > 32) stage at most 4 pieces: their kernels' piece loops stop there (a fifth
+// piece's bounds cost configs[3] 0.5-0.9 ms per step, profiles/r06z_five_pieces.txt)
+constexpr int STAGE_MAXP128 = 4;
+template <int KW>
+constexpr int stage_npc() { return KW == 2 ? STAGE_MAXP128 : STAGE_MAXP; }
 struct BucketSrc {
     const uint64_t *keys;
     int F;  // cell bits: a bucket's keys lie in [c0 << (2k-F), c1 << (2k-F))

@@ -118,13 +118,15 @@ def test_piece_counts_many_small_pieces(monkeypatch):
     assert_same_as_oracle(kc, oracle.OracleResult(fasta, 28, 10, 2048))
 
 
-@pytest.mark.parametrize("cuts,chunks", [("0.45,0.7,0.85", 0), ("0.3", 0), ("0.2,0.25,0.97", 0), ("0.4,0.7,0.9", 7)])
+@pytest.mark.parametrize("cuts,chunks", [("0.45,0.7,0.85", 0), ("0.3", 0), ("0.2,0.25,0.97", 0), ("0.4,0.7,0.9", 7),
+                                         ("0.3,0.55,0.75,0.9", 0)])
 def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, chunks):
     # a 1 GB job in one fk_ingest call (pinned): staged pieces at the job-size cuts (the
     # bench's path) against the same job counted whole from HBM (fk_ingest_device: no pieces),
     # every bin's keys and counts equal; a sampled slice of bins against the oracle is in
     # test_gpu_write; here both GPU paths must agree on all 2048 bins (a piece ends at its cut once it
-    # holds >= 128 MB: "0.2,0.25,0.97" cuts at 0.2, ~0.33 and 0.97)
+    # holds >= 128 MB: "0.2,0.25,0.97" cuts at 0.2, ~0.33 and 0.97; four cuts: five pieces, the
+    # schedule of 64-bit jobs of >= 4 GB)
     import torch
     n_reads = 1_000_000_000 // 114  # BASELINE configs[1]: pieces of >= 128 MB at every cut below
     dev = torch.empty(n_reads * 114, dtype=torch.uint8, device="cuda")
