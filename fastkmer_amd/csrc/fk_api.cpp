@@ -245,6 +245,10 @@ struct SortedPlan {
 
 }  // namespace
 
+#ifndef FK_SIDE_PRIO
+#define FK_SIDE_PRIO 1  // A/B builds: -DFK_SIDE_PRIO=0 the heavy tiers' stream at normal priority
+#endif
+
 struct fk_ctx {
     fk_config cfg{};
     int32_t Bc = 0;    // b = min(4^m, B)
@@ -264,6 +268,7 @@ struct fk_ctx {
     bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS=1: route every bucket through the streaming path
     uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: auto)
     int mid_parts = -1;        // FASTKMER_DEBUG_MID_PARTS: the mid tier's key ranges always (1) / never (0) / by size (-1)
+    bool split_retry = false;  // FASTKMER_DEBUG_SPLIT_RETRY: every split bucket cut a second time
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
     // Measurement-only (a library built with -DFK_PROBES; wrong results by design):
@@ -549,7 +554,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     c->W = cfg->k <= 32 ? 2 : 3;
     c->KW = cfg->k <= 32 ? 1 : 2;
     c->fm = make_fastmod((uint32_t)c->Bc);
-    // The product library reads eight variables: three sizes of the streamed input and five test
+    // The product library reads nine variables: three sizes of the streamed input and six test
     // hooks that steer small inputs onto paths only large or adversarial inputs reach (all
     // result-preserving).  Timing probes that alter results exist only in a library built with
     // -DFK_PROBES (python -m fastkmer_amd.build --probes).
@@ -577,6 +582,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *v = env("FASTKMER_DEBUG_LARGE_BUCKETS")) c->force_large = v[0] == '1';
     if (const char *v = env("FASTKMER_DEBUG_CELL_TARGET")) c->cell_target = (uint32_t)atoi(v);
     if (const char *v = env("FASTKMER_DEBUG_MID_PARTS")) c->mid_parts = atoi(v);  // test hook: 1 always, 0 never
+    if (const char *v = env("FASTKMER_DEBUG_SPLIT_RETRY")) c->split_retry = v[0] == '1';  // test hook
     if (const char *v = env("FASTKMER_X2_L1")) c->x2_l1 = atoi(v);
     if (const char *v = env("FASTKMER_FUSED")) c->fused = atoi(v);
 #ifdef FK_PROBES
@@ -614,7 +620,17 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     // later segments never queues behind a piece's expansion; the exchange: the received segments)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xstage, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xstage_ev, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->tier_side, hipStreamNonBlocking);
+    // the heavy tiers' stream at the device's highest priority (FK_SIDE_PRIO): their kernels are few
+    // and long chains (split, in-order sub-buckets, fallbacks with large workgroups), and at normal
+    // priority they waited for LDS behind the wave tier's millions of one-wave workgroups and ran
+    // alone after it (the configs[2] load's split fallbacks: 13.8 ms of a kernel of ~40 workgroups)
+    if (e == hipSuccess) {
+        int least = 0, greatest = 0;
+        if (FK_SIDE_PRIO && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+            e = hipStreamCreateWithPriority(&c->tier_side, hipStreamNonBlocking, greatest);
+        else
+            e = hipStreamCreateWithFlags(&c->tier_side, hipStreamNonBlocking);
+    }
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->side_ev[i], hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreate(&c->h2d_ev[i]);
     if (e != hipSuccess) {
@@ -1832,11 +1848,12 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                     HIP_TRY(launch_bucket_split64(src, B.buckets->as<Bucket>(), lists, 0, l1, nl,
                                                   c->sp_base.as<uint64_t>(), c->sp_keys.as<uint64_t>(),
                                                   c->sp_subs.as<SubBucket>(), c->sp_par.as<SplitParent>(), spc, fb,
-                                                  fb + nl, cap, k, F, hs));
+                                                  fb + nl, cap, k, F, hs, c->split_retry));
                 else
                     HIP_TRY(launch_bucket_split128(src, B.buckets->as<Bucket>(), l1, nl, c->sp_base.as<uint64_t>(),
                                                    c->sp_keys.as<uint64_t>(), c->sp_subs.as<SubBucket128>(),
-                                                   c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, hs));
+                                                   c->sp_par.as<SplitParent>(), spc, fb, fb + nl, cap, k, F, hs,
+                                                   c->split_retry));
                 HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 32, spc, 16, hipMemcpyDeviceToHost, hs));
                 HIP_TRY(hipEventRecord(c->tier_ev, hs));
                 HIP_TRY(hipEventSynchronize(c->tier_ev));

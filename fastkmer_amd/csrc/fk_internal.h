@@ -266,11 +266,12 @@ struct SplitParent {
 hipError_t launch_listed_sizes(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
                                uint32_t n1, uint64_t *sizes, hipStream_t s);
 // counts[0] += sub-buckets, counts[1] / [2] += buckets left to the block / big path (fb0 / fb1: their
-// indices; a bucket of n <= block_cap goes to fb0)
+// indices; a bucket of n <= block_cap goes to fb0).  A bucket whose cut leaves a sub-bucket above a
+// wave's keys is cut again from another sample into twice as many (retry: every bucket, a test hook)
 hipError_t launch_bucket_split64(const BucketSrc &src, const Bucket *buckets, const uint32_t *list0, uint32_t n0,
                                  const uint32_t *list1, uint32_t n1, const uint64_t *sbase, uint64_t *skeys,
                                  SubBucket *subs, SplitParent *parents, unsigned int *counts, uint32_t *fb0,
-                                 uint32_t *fb1, uint32_t block_cap, int k, int F, hipStream_t s);
+                                 uint32_t *fb1, uint32_t block_cap, int k, int F, hipStream_t s, bool retry = false);
 hipError_t launch_sub_count64_seq(const Bucket *buckets, const uint32_t *list, uint32_t nl, const SplitParent *parents,
                                   const SubBucket *subs, const uint64_t *skeys, uint64_t *out_keys,
                                   uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s, bool ordered);
@@ -284,7 +285,7 @@ struct SubBucket128 {
 hipError_t launch_bucket_split128(const BucketSrc &src, const Bucket *buckets, const uint32_t *list, uint32_t nl,
                                   const uint64_t *sbase, uint64_t *skeys, SubBucket128 *subs, SplitParent *parents,
                                   unsigned int *counts, uint32_t *fb0, uint32_t *fb1, uint32_t block_cap, int k, int F,
-                                  hipStream_t s);
+                                  hipStream_t s, bool retry = false);
 hipError_t launch_sub_count128_seq(const Bucket *buckets, const uint32_t *list, uint32_t nl, const SplitParent *parents,
                                    const SubBucket128 *subs, const uint64_t *skeys, uint64_t *out_keys,
                                    uint32_t *out_counts, uint64_t *bucket_unique, hipStream_t s, bool ordered);

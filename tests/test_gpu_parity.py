@@ -641,16 +641,22 @@ def test_grouped_emit_with_owners_set_after_map(k, m, B):
             assert np.array_equal(hi, rhi) and np.array_equal(lo, rlo) and np.array_equal(cnt, rcnt)
 
 
-@pytest.mark.parametrize("k,m,staged", [(28, 10, False), (32, 11, False), (21, 7, False), (28, 10, True),
-                                         (55, 12, False), (40, 9, False), (63, 15, False), (55, 12, True)])
-def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged):
+@pytest.mark.parametrize("k,m,staged,retry", [(28, 10, False, False), (32, 11, False, False), (21, 7, False, False),
+                                               (28, 10, True, False), (55, 12, False, False), (40, 9, False, False),
+                                               (63, 15, False, False), (55, 12, True, False), (28, 10, False, True),
+                                               (28, 10, True, True), (55, 12, False, True)])
+def test_heavy_bucket_split_vs_oracle(monkeypatch, k, m, staged, retry):
     # buckets above the wave tier (cells of a few thousand keys, FASTKMER_DEBUG_CELL_TARGET) split into
     # wave-sized sub-buckets by sampled splitters (~256 keys each), counted by the wave tier and
     # joined back in place -- from one key array and from staged pieces (a pinned ingest in 512 KB
     # pieces); k = 32 keys use all 64 bits; repeated reads leave sub-buckets too large for a wave, which
     # keep the block / big-table path (pieces need the fused map: k=28 m=10 or k=55 m=12); k > 32: the
-    # 128-bit split (k_bucket_split128 / k_sub_count128_seq), fallbacks to the LDS sort / streaming path
+    # 128-bit split (k_bucket_split128 / k_sub_count128_seq), fallbacks to the LDS sort / streaming path;
+    # retry (FASTKMER_DEBUG_SPLIT_RETRY): every bucket cut a second time from another sample into twice
+    # as many sub-buckets (the path of a bucket whose first cut left a sub-bucket above a wave's keys)
     monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", "2600")
+    if retry:
+        monkeypatch.setenv("FASTKMER_DEBUG_SPLIT_RETRY", "1")
     if staged:
         monkeypatch.setenv("FASTKMER_INGEST_SEG", str(256 << 10))
         monkeypatch.setenv("FASTKMER_PIECE_BYTES", str(512 << 10))
