@@ -267,7 +267,8 @@ struct fk_ctx {
     // Test hooks (result-preserving; they steer inputs that FASTA data cannot aim at onto a path):
     bool force_large = false;  // FASTKMER_DEBUG_LARGE_BUCKETS=1: route every bucket through the streaming path
     uint32_t cell_target = 0;  // FASTKMER_DEBUG_CELL_TARGET: average keys per cell of the largest bin (0: auto)
-    int mid_parts = -1;        // FASTKMER_DEBUG_MID_PARTS: the mid tier's key ranges always (1) / never (0) / by size (-1)
+    int mid_parts = -1;        // FASTKMER_DEBUG_MID_PARTS: the 64-bit mid tier's key ranges always (1), the whole
+                               // buckets on the 512-key table always (2), the 1024-key kernel only (0), by size (-1)
     bool split_retry = false;  // FASTKMER_DEBUG_SPLIT_RETRY: every split bucket cut a second time
     int x2_l1 = 0;             // FASTKMER_X2_L1: level-1 workgroup size (512, 1024; 0 = by fan-out)
     int fused = 1;             // FASTKMER_FUSED=0: two-kernel map (parse, then signature) for every input
@@ -581,7 +582,7 @@ FK_EXPORT int fk_create(const fk_config *cfg, fk_ctx **out) {
     if (const char *v = env("FASTKMER_INGEST_SEG")) c->ingest_seg = std::max(1ull << 16, strtoull(v, nullptr, 10));
     if (const char *v = env("FASTKMER_DEBUG_LARGE_BUCKETS")) c->force_large = v[0] == '1';
     if (const char *v = env("FASTKMER_DEBUG_CELL_TARGET")) c->cell_target = (uint32_t)atoi(v);
-    if (const char *v = env("FASTKMER_DEBUG_MID_PARTS")) c->mid_parts = atoi(v);  // test hook: 1 always, 0 never
+    if (const char *v = env("FASTKMER_DEBUG_MID_PARTS")) c->mid_parts = atoi(v);  // test hook: 1 / 2 / 0
     if (const char *v = env("FASTKMER_DEBUG_SPLIT_RETRY")) c->split_retry = v[0] == '1';  // test hook
     if (const char *v = env("FASTKMER_X2_L1")) c->x2_l1 = atoi(v);
     if (const char *v = env("FASTKMER_FUSED")) c->fused = atoi(v);
@@ -1818,17 +1819,25 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             // 64-bit mid tier: 2 or 3 key ranges per bucket on the wave tier's table (k_bucket_count64_parts);
             // the buckets it leaves (a range above 512 keys) are listed for the 1024-key kernel.  Only for a
             // large mid tier: the configs[2] load's 278 K mid buckets 146.5 -> 146.2 ms, but configs[1]'s 59 K
-            // 21.8 -> 21.95 ms (profiles/r06v_mid_parts_ab.txt)
-            const bool parts = FK_MID_PARTS && w1 && ntier[0] && block_top == WAVE_MID_CAP && c->mid_parts != 0 &&
-                               (c->mid_parts == 1 || ntier[0] >= MID_PARTS_MIN);
+            // 21.8 -> 21.95 ms (profiles/r06v_mid_parts_ab.txt).  A smaller mid tier (a job whose k-mers
+            // repeat: configs[1]) goes straight on the wave tier's table whole (k_bucket_count64_mid512), the
+            // buckets with more than 512 distinct keys listed for the 1024-key kernel.  Both run first on the
+            // side stream, ahead of the split.
+            const bool mid_wave = FK_MID_PARTS && w1 && ntier[0] && block_top == WAVE_MID_CAP && c->mid_parts != 0;
+            const bool parts = mid_wave && (c->mid_parts == 1 || (c->mid_parts != 2 && ntier[0] >= MID_PARTS_MIN));
             uint32_t *mid_fb = nullptr, nmidfb = 0;
             unsigned int *mid_fbc = c->misc.as<unsigned int>() + 11;
-            if (parts) {
+            if (mid_wave) {
                 FK_TRY(ensure(c->mid_fb, (uint64_t)ntier[0] * 4));
                 mid_fb = c->mid_fb.as<uint32_t>();
-                HIP_TRY(launch_bucket_count64_parts(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
-                                                    okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
-                                                    B.bucket_unique->as<uint64_t>(), mid_fb, mid_fbc, hs, ordered));
+                if (parts)
+                    HIP_TRY(launch_bucket_count64_parts(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                        okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                        B.bucket_unique->as<uint64_t>(), mid_fb, mid_fbc, hs, ordered));
+                else
+                    HIP_TRY(launch_bucket_count64_mid512(src, B.buckets->as<Bucket>(), lists, ntier[0], k,
+                                                         okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),
+                                                         B.bucket_unique->as<uint64_t>(), mid_fb, mid_fbc, hs, ordered));
             }
             if (FK_SPLIT_HEAVY && ntier[1]) {  // nothing to split: no split kernels, no read-back
                 const uint32_t nl = ntier[1];
@@ -1910,7 +1919,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 c->stats.split_buckets = nl - sc[1] - sc[2];
                 c->stats.sub_buckets = nsub;
             }
-            if (parts && !(FK_SPLIT_HEAVY && ntier[1])) {  // no split read-back: the fallbacks' count alone
+            if (mid_wave && !(FK_SPLIT_HEAVY && ntier[1])) {  // no split read-back: the fallbacks' count alone
                 HIP_TRY(hipMemcpyAsync(c->pin_tier.as<uint8_t>() + 44, mid_fbc, 4, hipMemcpyDeviceToHost, hs));
                 HIP_TRY(hipEventRecord(c->tier_ev, hs));
                 HIP_TRY(hipEventSynchronize(c->tier_ev));
@@ -1918,7 +1927,7 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
             }
             const uint32_t mid_cap = w1 ? WAVE_MID_CAP : WAVE128_MID_CAP;
             if (ntier[0]) {
-                if (parts) {
+                if (mid_wave) {
                     if (nmidfb)
                         HIP_TRY(launch_bucket_count64_wave_mid(src, B.buckets->as<Bucket>(), mid_fb, nmidfb, k,
                                                                okb.as<uint64_t>(), B.out_counts->as<uint32_t>(),

@@ -248,6 +248,12 @@ hipError_t launch_bucket_count64_parts(const BucketSrc &src, const Bucket *bucke
                                        uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
                                        uint64_t *bucket_unique, uint32_t *fb, unsigned int *fb_count, hipStream_t s,
                                        bool ordered);
+// the mid tier's buckets on the 512-key table when they hold <= 512 distinct keys (the others listed
+// in fb for the 1024-key kernel): a job whose k-mers repeat
+hipError_t launch_bucket_count64_mid512(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
+                                        uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,
+                                        uint64_t *bucket_unique, uint32_t *fb, unsigned int *fb_count, hipStream_t s,
+                                        bool ordered);
 // the listed block-tier buckets of at most WAVE_MID_CAP keys, one wave each (k <= 32)
 hipError_t launch_bucket_count64_wave_mid(const BucketSrc &src, const Bucket *buckets, const uint32_t *list,
                                           uint64_t nlist, int k, uint64_t *out_keys, uint32_t *out_counts,

@@ -449,17 +449,22 @@ def test_block_and_big_tiers_vs_oracle(monkeypatch):
     assert_same_as_oracle(kc, ref)
 
 
-@pytest.mark.parametrize("cell_target,staged,use_ht", [(700, False, False), (700, True, False), (700, False, True),
-                                                      (400, False, False)])
-def test_mid_tier_key_ranges_vs_oracle(monkeypatch, cell_target, staged, use_ht):
-    # cells of ~700 (~400) keys: many buckets of 513..1024 keys, which the 64-bit mid tier counts as 2 or 3
-    # key ranges on the wave tier's table (k_bucket_count64_parts); 600 copies of a few reads put k-mers
-    # repeated 600 times into some of them, a range above 512 keys that the 1024-key kernel takes over
+@pytest.mark.parametrize("cell_target,staged,use_ht,mode,genome", [
+    (700, False, False, 1, 3_000_000_000), (700, True, False, 1, 3_000_000_000), (700, False, True, 1, 3_000_000_000),
+    (400, False, False, 1, 3_000_000_000), (700, False, False, 2, 2_000_000), (700, True, False, 2, 2_000_000),
+    (700, False, True, 2, 2_000_000), (700, False, False, 2, 3_000_000_000)])
+def test_mid_tier_key_ranges_vs_oracle(monkeypatch, cell_target, staged, use_ht, mode, genome):
+    # cells of ~700 (~400) keys: many buckets of 513..1024 keys.  mode 1: the 64-bit mid tier counts them
+    # as 2 or 3 key ranges on the wave tier's table (k_bucket_count64_parts); 600 copies of a few reads
+    # put k-mers repeated 600 times into some of them, a range above 512 keys that the 1024-key kernel
+    # takes over.  mode 2: whole on the wave tier's table (k_bucket_count64_mid512) -- reads of a 2 Mbp
+    # genome (10x: ~100 distinct keys per bucket), and of a 3 Gbp one, whose buckets hold more than 512
+    # distinct keys and give up to the 1024-key kernel
     monkeypatch.setenv("FASTKMER_DEBUG_CELL_TARGET", str(cell_target))
-    monkeypatch.setenv("FASTKMER_DEBUG_MID_PARTS", "1")  # the product takes the ranges kernel from 2^17 mid buckets
+    monkeypatch.setenv("FASTKMER_DEBUG_MID_PARTS", str(mode))  # the product picks by the mid tier's size
     rep = b"".join(b">r%d\n" % i + b"GATTACAGGCATCGATCGGGCTAGCTAGGCTAGCTTACGAGCTAGCATCGACTAGCATGCATGCATCGACGTAGCATCG"
                    b"ACGTTGCAAGGCTTACCGATCGG\n" for i in range(600))
-    fasta = fk.synth_fasta(200_000, 100, 3_000_000_000, seed=0x7A + cell_target) + rep
+    fasta = fk.synth_fasta(200_000, 100, genome, seed=0x7A + cell_target) + rep
     if staged:
         import torch
         monkeypatch.setenv("FASTKMER_INGEST_SEG", str(1 << 20))
