@@ -2422,7 +2422,10 @@ static int staged_count(fk_ctx *c) {
 // size: every piece_bytes, at most three pieces before fk_finish stages the last one (with cuts: at
 // most stage_maxp - 1).
 static bool local_piece_due(const fk_ctx *c, uint64_t tiles) {
-    constexpr uint64_t MIN_PIECE = 256ull << 20;
+#ifndef FK_MIN_PIECE_MB
+#define FK_MIN_PIECE_MB 256  // A/B builds: a piece holds >= half of it
+#endif
+    constexpr uint64_t MIN_PIECE = (uint64_t)FK_MIN_PIECE_MB << 20;
     if (c->st_np >= stage_maxp(c) - 1) return false;
     const uint64_t tile = fm_tile_bytes(FUSED_NT);
     if (c->job_bytes && !c->piece_bytes_set) {
