@@ -1844,13 +1844,15 @@ static int sorted_count_buckets(fk_ctx *c, const SortedPlan &pl, const BucketSrc
                 const uint64_t maxsub = listed_keys / 64 + nl + 64;  // >= ceil(n / SPL_TGT) sub-buckets per bucket
                 const size_t sub_bytes = w1 ? sizeof(SubBucket) : sizeof(SubBucket128);
                 FK_TRY(ensure(c->sp_base, ((uint64_t)nl + 1) * 8));
-                FK_TRY(ensure(c->sp_keys, listed_keys * 8 * c->KW));
+                // 64-bit keys: a 512-key region per first-cut sub-bucket (split_room: <= 2 n + 512 per bucket)
+                FK_TRY(ensure(c->sp_keys, (w1 ? 2 * listed_keys + 512ull * nl : listed_keys) * 8 * c->KW));
                 FK_TRY(ensure(c->sp_subs, maxsub * sub_bytes));
                 FK_TRY(ensure(c->sp_par, (uint64_t)nl * sizeof(SplitParent)));
                 FK_TRY(ensure(c->sp_fb, (uint64_t)nl * 8));
                 uint32_t *fb = c->sp_fb.as<uint32_t>();
                 unsigned int *spc = c->misc.as<unsigned int>() + 8;  // [0] sub-buckets, [1] / [2] fallbacks
-                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(), hs));
+                HIP_TRY(launch_listed_sizes(B.buckets->as<Bucket>(), lists, 0, l1, nl, c->sp_base.as<uint64_t>(), hs,
+                                            w1));
                 HIP_TRY(scan_excl_sum_u64(c->sp_base.as<uint64_t>(), c->sp_base.as<uint64_t>(), nl,
                                           c->sp_base.as<uint64_t>() + nl, c->ws, hs));
                 if (w1)

@@ -268,9 +268,11 @@ struct SubBucket {
 struct SplitParent {
     uint32_t first, nsub;  // sub-buckets [first, first + nsub) of the list; nsub = 0: not split
 };
-// sizes[i] = n of listed bucket i (list0 then list1)
+// sizes[i] = the room of listed bucket i (list0 then list1) in the split copy: its keys, or with slots
+// (64-bit keys) split_room: a 512-key region per first-cut sub-bucket
 hipError_t launch_listed_sizes(const Bucket *buckets, const uint32_t *list0, uint32_t n0, const uint32_t *list1,
-                               uint32_t n1, uint64_t *sizes, hipStream_t s);
+                               uint32_t n1, uint64_t *sizes, hipStream_t s,
+                               bool slots = false);
 // counts[0] += sub-buckets, counts[1] / [2] += buckets left to the block / big path (fb0 / fb1: their
 // indices; a bucket of n <= block_cap goes to fb0).  A bucket whose cut leaves a sub-bucket above a
 // wave's keys is cut again from another sample into twice as many (retry: every bucket, a test hook)
