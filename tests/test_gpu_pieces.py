@@ -159,3 +159,32 @@ def test_staged_job_cuts_vs_one_count(monkeypatch, cuts, chunks):
         assert np.array_equal(ka, kb) and np.array_equal(ca, cb), f"bin {bin_}"
     a.close()
     b.close()
+
+
+def test_staged_job_cuts_128bit_keys_at_most_four_pieces(monkeypatch):
+    # k > 32 keys stage at most four pieces (their kernels' piece loops stop there, stage_npc): four
+    # cuts give four pieces, the last one taking the rest; every bin equal to the job counted whole
+    # from HBM (fk_ingest_device: no pieces)
+    import torch
+    n_reads = 700_000_000 // 164  # 150 bp reads: pieces of >= 128 MB at each cut kept
+    dev = torch.empty(n_reads * 164, dtype=torch.uint8, device="cuda")
+    fk.synth_fasta_to_device(dev.data_ptr(), n_reads, 150, 100_000_000, seed=0x5EED)
+    host = torch.empty(dev.numel(), dtype=torch.uint8).pin_memory()
+    host.copy_(dev)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("FASTKMER_PIECE_CUTS", "0.3,0.55,0.75,0.9")
+    a = fk.KmerCounter(55, 12, 3, 1024)
+    a.ingest_ptr(host.data_ptr(), host.numel())
+    a.finish()
+    assert a.stats()["pieces_counted"] == 4
+    b = fk.KmerCounter(55, 12, 3, 1024)
+    b.ingest_device(dev.data_ptr(), dev.numel())
+    b.finish()
+    assert a.stats()["kmers"] == b.stats()["kmers"] and a.stats()["distinct"] == b.stats()["distinct"]
+    assert np.array_equal(a.bin_sizes(), b.bin_sizes())
+    for bin_ in range(0, 1024, 7):
+        ka, ca = a.get_bin(bin_)
+        kb, cb = b.get_bin(bin_)
+        assert np.array_equal(ka, kb) and np.array_equal(ca, cb), f"bin {bin_}"
+    a.close()
+    b.close()
